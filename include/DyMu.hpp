@@ -1,0 +1,131 @@
+// DyMu.hpp -- PathPlanning_lib::DyMuPathPlanner, the global-layer surface of
+// the reference class (src/DyMu.hpp:397-609) re-implemented over row-major
+// SoA arrays, with the total-cost propagation delegated to the MI355X engine
+// through the C-ABI in dymu_fim.h.
+//
+// Same method names, argument meaning and return values as the reference for
+// the hot path and its two neighbours (cost-map ingestion, path extraction):
+//   initGlobalLayer      src/DyMu_GlobalPathPlanning.cpp:39-104
+//   setCostMap           :109-126
+//   computeCostMap       :145-181 (+ :186-308, quirks Q1-Q4 of SURVEY s8(a))
+//   setGoal              :322-357
+//   computeTotalCostMap  :364-408
+//   computeEntireTotalCostMap :443-468
+//   getPath / computeGlobalPath :589-662 (+ :666-784)
+//   getTotalCostMatrix, getGlobalCostMatrix, getHazardDensityMatrix,
+//   getTrafficabilityMatrix, getTotalCost, getLocomotionMode  :788-890
+// Differences a caller can see:
+//   * the local (sub-grid) layer, CoRa and risk methods are not part of this
+//     library (out of scope); getPath's evaluatePath(0) is then the
+//     identity, as in the reference when no local map exists.
+//   * computeTotalCostMap solves the whole map (the reference stops at the
+//     start node); every reachable cell holds its converged value.
+//   * the node-pointer members (global_narrowband, global_propagated_nodes,
+//     global_goal as globalNode*) do not exist: nodes are SoA arrays.
+//   * a start or goal on the border returns false instead of dereferencing
+//     NULL (reference :416-417, :430-431).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "dymu_base.hpp"
+#include "dymu_fim.h"
+
+namespace PathPlanning_lib {
+
+enum node_state { OPEN, CLOSED };
+
+enum repairingAproach {
+  CONSERVATIVE,  // Hazard Avoidance - FM*
+  SWEEPING       // multiBiFM*
+};
+
+class DyMuPathPlanner {
+ public:
+  // -- public state kept from the reference (src/DyMu.hpp:444-467) --
+  std::vector<base::Waypoint> current_path;  // the last computed path
+  std::vector<double> cost_lutable;          // cost LUT (computeCostMap)
+  double remaining_total_cost = 0.0;
+  int reconnecting_index = 0;
+
+  DyMuPathPlanner(double risk_distance, double reconnect_distance, double risk_ratio,
+                  repairingAproach input_approach);
+  ~DyMuPathPlanner();
+  DyMuPathPlanner(const DyMuPathPlanner&) = delete;
+  DyMuPathPlanner& operator=(const DyMuPathPlanner&) = delete;
+
+  bool initGlobalLayer(double globalres, double localres, unsigned num_nodes_X,
+                       unsigned num_nodes_Y, std::vector<double> offset);
+  bool setCostMap(std::vector<std::vector<double>> cost_map);
+  bool computeCostMap(std::vector<double> cost_data, std::vector<double> slope_values,
+                      std::vector<std::string> locomotionModes,
+                      std::vector<std::vector<double>> elevation,
+                      std::vector<std::vector<double>> terrainMap);
+
+  bool setGoal(base::Waypoint wGoal);
+  bool computeTotalCostMap(base::Waypoint wPos);
+  bool computeEntireTotalCostMap();
+
+  std::vector<base::Waypoint> getPath(base::Waypoint wPos);
+  bool computeGlobalPath(base::Waypoint wPos);
+  base::Waypoint computeNextGlobalWaypoint(base::Waypoint& wPos, double tau);
+  double interpolate(double a, double b, double g00, double g01, double g10, double g11);
+
+  std::string getLocomotionMode(base::Waypoint wPos);
+  std::vector<std::vector<double>> getTotalCostMatrix();
+  std::vector<std::vector<double>> getGlobalCostMatrix();
+  std::vector<std::vector<double>> getHazardDensityMatrix();
+  std::vector<std::vector<double>> getTrafficabilityMatrix();
+  double getTotalCost(base::Waypoint wInt);
+
+  // -- extensions (not in the reference) --
+  // Flat row-major views for FFI callers (ny*nx, index j*nx + i).
+  const double* totalCostData() const { return total_cost_.data(); }
+  unsigned sizeX() const { return nx_; }
+  unsigned sizeY() const { return ny_; }
+  bool hasGoal() const { return has_goal_; }
+  unsigned goalI() const { return goal_i_; }
+  unsigned goalJ() const { return goal_j_; }
+  const dymu_stats& lastStats() const { return stats_; }
+  // Local-layer feedback on the global layer (the writes of
+  // src/DyMu_LocalPathRepairing.cpp:264-274 and :389-394), row-major ny*nx.
+  bool setHazardDensity(const std::vector<double>& hd);
+  bool setTrafficability(const std::vector<double>& tr);
+  // Engine options (device ordinal etc.); takes effect on the next solve.
+  void setEngineOptions(const dymu_opts& o);
+
+ private:
+  uint64_t idx(unsigned i, unsigned j) const { return (uint64_t)j * nx_ + i; }
+  bool solveFull();  // pack F, run the engine, unpack T / state
+  void gradientNode(unsigned i, unsigned j, double& dnx, double& dny) const;
+  bool isSafeNode(unsigned i, unsigned j) const;
+
+  // parameters (src/DyMu.hpp:399-427)
+  double risk_distance_, reconnect_distance_, risk_ratio_;
+  repairingAproach repairing_approach_;
+  unsigned nx_ = 0, ny_ = 0;
+  double global_res_ = 1.0, local_res_ = 1.0;
+  std::vector<double> global_offset_{0.0, 0.0};
+  std::vector<double> slope_range_;
+  std::vector<std::string> locomotion_modes_;
+
+  // SoA node fields (globalNode, src/DyMu.hpp:69-108)
+  std::vector<double> elevation_, slope_, raw_cost_, cost_, hazard_, traff_, total_cost_;
+  std::vector<uint32_t> terrain_;
+  std::vector<uint8_t> is_obstacle_, state_;
+  std::vector<int32_t> loc_mode_;  // -1 = "DONT_CARE"
+  std::vector<double> heading_unused_;
+
+  bool has_goal_ = false;
+  unsigned goal_i_ = 0, goal_j_ = 0;
+  double goal_heading_ = 0.0;
+
+  dymu_ctx* ctx_ = nullptr;
+  dymu_opts opts_{-1, 0, 0, 0, 0};
+  dymu_stats stats_{};
+  std::vector<double> speed_;  // packed F
+};
+
+}  // namespace PathPlanning_lib

@@ -1,0 +1,119 @@
+/*
+ * dymu_fim.h -- C-ABI of the MI355X (gfx950) total-cost propagation engine.
+ *
+ * This is the drop-in boundary for the DyMu global total-cost propagation
+ * (ESA-PRL/planning-path_planning).  It replaces, for the host C++ planner
+ * (include/DyMu.hpp), the hot loop of:
+ *   - DyMuPathPlanner::computeEntireTotalCostMap   src/DyMu_GlobalPathPlanning.cpp:443-468
+ *   - DyMuPathPlanner::computeTotalCostMap         src/DyMu_GlobalPathPlanning.cpp:364-408
+ *   - propagateGlobalNode (Eikonal update)          src/DyMu_GlobalPathPlanning.cpp:500-546
+ *   - minCostGlobalNode (narrow band)               src/DyMu_GlobalPathPlanning.cpp:551-568
+ *   - resetTotalCostMap / resetGlobalNarrowBand     src/DyMu_GlobalPathPlanning.cpp:473-496
+ * The reference has no FFI; its boundary is the C++ class in src/DyMu.hpp:397-609.
+ * This header is the C surface that class (our include/DyMu.hpp) calls, and
+ * the one a cgo / JNI / ctypes binding would bind.
+ *
+ * Data model: row-major fp64 grids, index = j*ld + i (j = y row, i = x col,
+ * reference :52-58).  F[k] is the per-node speed C of reference :527-528,
+ *   F = global_res * cost * (2 + hazard_density - trafficability),
+ * and +inf (or NaN) for an obstacle.  F must be >= 0 or +inf.  T[k] receives
+ * the converged total cost; +inf marks unreachable cells and obstacles; the
+ * goal holds 0.  Results equal the reference FMM within |dT| <= 1e-12*max(1,T)
+ * with an identical +inf mask.
+ *
+ * All functions return DYMU_OK (0) or a negative dymu_status.  Contexts are
+ * not thread-safe; use one context per host thread.
+ */
+#ifndef DYMU_FIM_H
+#define DYMU_FIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DYMU_ABI_VERSION 1
+
+typedef enum dymu_status {
+  DYMU_OK = 0,
+  DYMU_ERR_ARG = -1,           /* bad argument (null pointer, size, goal off-grid) */
+  DYMU_ERR_HIP = -2,           /* HIP runtime error (see dymu_last_error) */
+  DYMU_ERR_NOMEM = -3,         /* device allocation failed */
+  DYMU_ERR_NOT_CONVERGED = -4, /* pass cap reached (dymu_opts.max_passes) */
+  DYMU_ERR_NO_DEVICE = -5,     /* no HIP device / extension unusable */
+  DYMU_ERR_RCCL = -6,          /* RCCL error in the sharded solver */
+  DYMU_ERR_STATE = -7          /* call out of sequence (e.g. comm not initialised) */
+} dymu_status;
+
+typedef struct dymu_ctx dymu_ctx;
+
+typedef struct dymu_opts {
+  int device;           /* HIP device ordinal; -1 = current device */
+  int passes_per_check; /* passes launched between convergence read-backs; 0 = adaptive */
+  int max_passes;       /* safety cap on FIM passes; 0 = derived from the grid size */
+  int max_inner;        /* cap on in-tile sweeps per tile visit; 0 = default */
+  int grid_blocks;      /* workgroups per pass launch; 0 = derived from the device */
+} dymu_opts;
+
+typedef struct dymu_stats {
+  uint64_t passes;       /* FIM passes that had active tiles ("iterations to converge") */
+  uint64_t launches;     /* pass kernels launched (incl. speculative empty ones) */
+  uint64_t tile_visits;  /* sum over passes of active tiles */
+  uint64_t inner_sweeps; /* sum over tile visits of in-tile sweeps */
+  uint64_t max_active;   /* largest active-tile list */
+  uint64_t rounds;       /* sharded solver: halo-exchange rounds (0 single GPU) */
+  double ms;             /* device time of the solve (HIP events), ms */
+  int tile_w, tile_h;    /* tile geometry used */
+} dymu_stats;
+
+/* Context: owns a HIP stream, events and workspace on one device. */
+int dymu_create(dymu_ctx** out, const dymu_opts* opts); /* opts may be NULL */
+int dymu_destroy(dymu_ctx* ctx);
+
+/* Host-buffer solve: copies F in, solves, copies T out (the planner path).
+ * F, T_out: nx*ny doubles, row-major, caller-owned host memory. */
+int dymu_solve(dymu_ctx* ctx, const double* F, uint32_t nx, uint32_t ny, uint32_t goal_i,
+               uint32_t goal_j, double* T_out, dymu_stats* stats);
+
+/* Device-resident solve: dF, dT are device pointers with row pitch `ld`
+ * elements (ld >= nx).  dT is overwritten (initialised to +inf, goal 0).
+ * `stream` is a hipStream_t or NULL for the context's own stream.  Blocks
+ * until converged. */
+int dymu_solve_device(dymu_ctx* ctx, const double* dF, double* dT, uint32_t nx, uint32_t ny,
+                      uint64_t ld, uint32_t goal_i, uint32_t goal_j, void* stream,
+                      dymu_stats* stats);
+
+/* Synthetic input generator on the device (bench/test data):
+ *   F[k] = 1 + 4*u(seed, k),  u(s,k) = (splitmix64(s ^ k) >> 11) * 2^-53,
+ *   obstacle (F = +inf) where u(obst_seed, k) < obst_frac, except the 3x3
+ *   block around (goal_i, goal_j).  k = j*nx + i is the GLOBAL cell index, so
+ *   shards generate identical values: rows [row0, row0+ny) of a grid nx wide. */
+int dymu_synth_speed(dymu_ctx* ctx, double* dF, uint32_t nx, uint32_t ny, uint64_t ld,
+                     uint64_t row0, uint64_t seed, double obst_frac, uint64_t obst_seed,
+                     uint32_t goal_i, uint32_t goal_j, void* stream);
+
+/* Device memory helpers (so a host without torch can run the device path). */
+int dymu_device_alloc(dymu_ctx* ctx, size_t bytes, void** dptr);
+int dymu_device_free(dymu_ctx* ctx, void* dptr);
+int dymu_memcpy_d2h(dymu_ctx* ctx, void* dst, const void* src, size_t bytes);
+int dymu_memcpy_h2d(dymu_ctx* ctx, void* dst, const void* src, size_t bytes);
+
+/* Profiling: when on, every pass launch is bracketed by HIP events so
+ * dymu_last_pass_timing() reports pure kernel time (adds event overhead). */
+int dymu_set_profiling(dymu_ctx* ctx, int on);
+
+/* Kernel time of the most recent solve's pass launches (ms, HIP events on
+ * the launch stream) and their count -- the bench's roofline source. */
+int dymu_last_pass_timing(dymu_ctx* ctx, double* pass_ms_total, uint64_t* n_pass_launches);
+
+const char* dymu_strerror(int status);
+const char* dymu_last_error(dymu_ctx* ctx); /* last HIP/RCCL error text */
+int dymu_abi_version(void);
+int dymu_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,75 @@
+/*
+ * dymu_planner.h -- flat C-ABI over PathPlanning_lib::DyMuPathPlanner
+ * (include/DyMu.hpp) for non-C++ callers (ctypes, cgo, JNI).
+ *
+ * Each entry point forwards to the class method of the same name, which in
+ * turn follows the reference method cited in DyMu.hpp.  Boolean methods
+ * return 1 (true) / 0 (false); a negative value is a dymu_status error (for
+ * example DYMU_ERR_NO_DEVICE when the HIP engine cannot run).  Grids are
+ * row-major ny*nx doubles, index j*nx + i.  Waypoints are (x, y, z, heading).
+ */
+#ifndef DYMU_PLANNER_H
+#define DYMU_PLANNER_H
+
+#include <stdint.h>
+
+#include "dymu_fim.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dymu_planner dymu_planner;
+
+/* DyMuPathPlanner(risk_distance, reconnect_distance, risk_ratio, approach)
+ * (reference src/DyMu_GlobalPathPlanning.cpp:22-33); approach 0 CONSERVATIVE, 1 SWEEPING */
+int dymu_planner_create(dymu_planner** out, double risk_distance, double reconnect_distance,
+                        double risk_ratio, int approach);
+void dymu_planner_destroy(dymu_planner* p);
+int dymu_planner_set_engine_options(dymu_planner* p, const dymu_opts* opts);
+
+/* initGlobalLayer (:39-104) */
+int dymu_planner_init_global_layer(dymu_planner* p, double globalres, double localres,
+                                   uint32_t nx, uint32_t ny, double offx, double offy);
+/* setCostMap (:109-126); cost_map: ny*nx */
+int dymu_planner_set_cost_map(dymu_planner* p, const double* cost_map, uint32_t nx, uint32_t ny);
+/* computeCostMap (:145-181); loc_modes: n_locs C strings */
+int dymu_planner_compute_cost_map(dymu_planner* p, const double* lut, int lut_len,
+                                  const double* slopes, int n_slopes, const char* const* loc_modes,
+                                  int n_locs, const double* elevation, const double* terrain);
+/* setGoal (:322-357) */
+int dymu_planner_set_goal(dymu_planner* p, double x, double y, double z, double heading);
+/* computeTotalCostMap (:364-408) */
+int dymu_planner_compute_total_cost_map(dymu_planner* p, double x, double y, double z,
+                                        double heading);
+/* computeEntireTotalCostMap (:443-468) */
+int dymu_planner_compute_entire_total_cost_map(dymu_planner* p);
+
+/* getTotalCostMatrix (:799-811, +inf -> -1), getGlobalCostMatrix (:815-829),
+ * getHazardDensityMatrix (:833-842), getTrafficabilityMatrix (:846-855) */
+int dymu_planner_get_total_cost_matrix(dymu_planner* p, double* out);
+int dymu_planner_get_global_cost_matrix(dymu_planner* p, double* out);
+int dymu_planner_get_hazard_density_matrix(dymu_planner* p, double* out);
+int dymu_planner_get_trafficability_matrix(dymu_planner* p, double* out);
+/* raw total cost (+inf unreachable), ny*nx */
+int dymu_planner_get_total_cost_raw(dymu_planner* p, double* out);
+/* getTotalCost(Waypoint) (:860-890) */
+int dymu_planner_get_total_cost(dymu_planner* p, double x, double y, double z, double heading,
+                                double* out);
+/* getPath (:589-611): writes up to max_wp waypoints (x,y,z,heading); returns
+ * the number of waypoints (>= 0) or a negative status */
+int dymu_planner_get_path(dymu_planner* p, double x, double y, double z, double heading,
+                          double* out_xyzh, int max_wp);
+/* getLocomotionMode (:788-795) into buf (NUL-terminated) */
+int dymu_planner_get_locomotion_mode(dymu_planner* p, double x, double y, double z, double heading,
+                                     char* buf, int buflen);
+/* dynamic feedback (extension): hazard_density / trafficability, ny*nx */
+int dymu_planner_set_hazard_density(dymu_planner* p, const double* hd);
+int dymu_planner_set_trafficability(dymu_planner* p, const double* tr);
+/* statistics of the last solve */
+int dymu_planner_last_stats(dymu_planner* p, dymu_stats* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,295 @@
+// fim_kernels.hip -- MI355X (gfx950) block Fast-Iterative-Method kernels for the
+// DyMu global total-cost propagation (reference: src/DyMu_GlobalPathPlanning.cpp).
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (no FMA contraction:
+// every update rounds exactly like the reference's SSE2 build).
+//
+// Algorithm: the grid is cut into TB_W x TB_H tiles.  A pass
+// kernel walks the device-built list of active tiles; each workgroup loads one
+// tile of T (plus a 1-cell halo) into LDS and the tile's F into registers,
+// relaxes the reference's Eikonal update (:500-546) in place until the tile is
+// locally converged, writes back the cells that decreased and enqueues the
+// neighbour tiles whose shared edge changed.  Values only decrease, every
+// update is the reference's exact arithmetic, so the converged map is the
+// fixed point the reference FMM reaches.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fim_kernels.h"
+
+namespace dymu {
+
+__device__ __forceinline__ double dinf() { return __builtin_inf(); }
+
+// Reference :504-535.  Tx = fmin(W,E), Ty = fmin(N,S); off-grid neighbours
+// are +inf (a NULL nb4 makes the reference use the other one alone, :508-523).
+// 2*pow(C,2.0) - pow(Tx-Ty,2.0) with pow(x,2.0) == x*x; no contraction.
+__device__ __forceinline__ double eikonal(double tx, double ty, double c) {
+  const double d = tx - ty;
+  if ((fabs(d) < c) && (tx < dinf()) && (ty < dinf())) {
+    const double cc = c * c;
+    const double r = 2.0 * cc - d * d;
+    return (tx + ty + sqrt(r)) / 2;
+  }
+  return fmin(tx, ty) + c;
+}
+
+// ---------------------------------------------------------------------------
+// T initialisation: +inf everywhere, 0 at the goal (resetTotalCostMap +
+// resetGlobalNarrowBand, :473-496).  Ghost rows (sharded mode) are included
+// when rows < 0 / >= ny are passed in.
+// ---------------------------------------------------------------------------
+__global__ void k_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, int64_t row_hi) {
+  const uint64_t rows = (uint64_t)(row_hi - row_lo);
+  const uint64_t n = rows * nx;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+       k += (uint64_t)gridDim.x * blockDim.x) {
+    const int64_t r = row_lo + (int64_t)(k / nx);
+    const uint64_t c = k % nx;
+    T[r * (int64_t)ld + (int64_t)c] = dinf();
+  }
+}
+
+__global__ void k_seed(double* T, uint64_t ld, int64_t gi, int64_t gj, uint32_t* list,
+                       uint32_t* count, uint32_t* tile_epoch, uint32_t epoch, uint32_t tile,
+                       int set_goal) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    if (set_goal) T[gj * (int64_t)ld + gi] = 0.0;
+    if (atomicMax(&tile_epoch[tile], epoch) < epoch) {
+      const uint32_t pos = atomicAdd(count, 1u);
+      list[pos] = tile;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The pass kernel.
+// Thread layout: 256 threads = 32 columns x 8 strips; thread (c, s) owns the
+// 4 cells of column c, rows 4s..4s+3 of the tile, in registers.  The tile's
+// T lives in LDS with a 1-cell halo so horizontal and strip-boundary
+// neighbours are LDS reads; a strip's own vertical neighbours are registers.
+// Sweeps alternate upward / downward inside a strip (Gauss-Seidel within the
+// strip, chaotic in-place across threads: every value read is an upper bound
+// of the fixed point, so any interleaving converges to it).
+// ---------------------------------------------------------------------------
+constexpr int TW = kTileW;  // 32
+constexpr int TH = kTileH;  // 32
+constexpr int RPT = TH / 8; // rows per thread = 4
+constexpr int LDS_W = TW + 2;
+
+// One cell of a strip: neighbours from registers (same strip) or LDS.
+__device__ __forceinline__ bool relax_cell(double (*sT)[LDS_W], double (&t)[RPT],
+                                           const double (&f)[RPT], int s, int c, int k) {
+  const int r = s * RPT + k;
+  const double south = (k == 0) ? sT[r][c + 1] : t[k - 1];
+  const double north = (k == RPT - 1) ? sT[r + 2][c + 1] : t[k + 1];
+  const double west = sT[r + 1][c];
+  const double east = sT[r + 1][c + 2];
+  const double u = eikonal(fmin(west, east), fmin(north, south), f[k]);  // :506, :519
+  if (u < t[k]) {                                                        // :537
+    t[k] = u;
+    sT[r + 1][c + 1] = u;
+    return true;
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(256) void k_fim_pass(PassArgs a) {
+  __shared__ double sT[TH + 2][LDS_W];
+  __shared__ unsigned s_edge;
+
+  const int tid = threadIdx.x;
+  const int c = tid & (TW - 1);  // column in tile
+  const int s = tid >> 5;        // strip 0..7
+  const uint32_t n_active = *a.count_in;
+
+  if (blockIdx.x == 0 && tid == 0) {
+    *a.count_clear = 0u;  // list (p+2)%3: read by pass p-1 (finished), appended by pass p+1
+    if (n_active > 0) {
+      atomicAdd(&a.stats[kStatPasses], 1ull);
+      atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
+    }
+  }
+
+  for (uint32_t li = blockIdx.x; li < n_active; li += gridDim.x) {
+    const uint32_t tile = a.list_in[li];
+    const int tx = (int)(tile % (uint32_t)a.ntx);
+    const int ty = (int)(tile / (uint32_t)a.ntx);
+    const int64_t i0 = (int64_t)tx * TW;
+    const int64_t j0 = (int64_t)ty * TH;
+    const int64_t gi = i0 + c;
+    const bool col_ok = gi < a.nx;
+
+    if (tid == 0) s_edge = 0u;
+
+    // ---- load own cells: T into registers + LDS, F into registers ----
+    double t[RPT], f[RPT], t0[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int r = s * RPT + k;
+      const int64_t gj = j0 + r;
+      double tv = dinf(), fv = dinf();
+      if (col_ok && gj < a.ny) {
+        const int64_t off = gj * (int64_t)a.ld + gi;
+        tv = a.T[off];
+        fv = a.F[off];
+      }
+      t[k] = tv;
+      t0[k] = tv;
+      f[k] = fv;
+      sT[r + 1][c + 1] = tv;
+    }
+    // ---- halo: rows -1 / TH (threads 0..31 / 32..63), cols -1 / TW (64..127) ----
+    if (tid < 64) {
+      const int hc = tid & 31;
+      const bool top = tid >= 32;
+      const int64_t gj = top ? j0 + TH : j0 - 1;
+      const int64_t gii = i0 + hc;
+      double v = dinf();
+      const bool row_ok = top ? (gj < a.ny || (gj == a.ny && a.ghost_hi))
+                              : (gj >= 0 || a.ghost_lo);
+      if (row_ok && gii < a.nx) v = a.T[gj * (int64_t)a.ld + gii];
+      sT[top ? TH + 1 : 0][hc + 1] = v;
+    } else if (tid < 128) {
+      const int hr = tid & 31;
+      const bool right = tid >= 96;
+      const int64_t gii = right ? i0 + TW : i0 - 1;
+      const int64_t gj = j0 + hr;
+      double v = dinf();
+      if (gii >= 0 && gii < a.nx && gj < a.ny) v = a.T[gj * (int64_t)a.ld + gii];
+      sT[hr + 1][right ? TW + 1 : 0] = v;
+    }
+    __syncthreads();
+
+    // ---- relax to local convergence ----
+    int sweeps = 0;
+    bool capped = true;
+    for (; sweeps < a.max_inner;) {
+      bool changed = false;
+      // alternate upward / downward order inside the strip; both loops are
+      // fully unrolled so t[] / f[] stay in registers (no dynamic indexing)
+      if ((sweeps & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) changed |= relax_cell(sT, t, f, s, c, k);
+      } else {
+#pragma unroll
+        for (int k = RPT - 1; k >= 0; --k) changed |= relax_cell(sT, t, f, s, c, k);
+      }
+      ++sweeps;
+      if (!__syncthreads_or(changed)) {
+        capped = false;
+        break;
+      }
+    }
+
+    // ---- write back + edge-change flags ----
+    unsigned edge = 0u;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int r = s * RPT + k;
+      if (t[k] < t0[k]) {
+        const int64_t gj = j0 + r;
+        a.T[gj * (int64_t)a.ld + gi] = t[k];
+        if (r == 0) edge |= 1u;       // south neighbour tile (nb4[0])
+        if (c == 0) edge |= 2u;       // west  (nb4[1])
+        if (c == TW - 1) edge |= 4u;  // east  (nb4[2])
+        if (r == TH - 1) edge |= 8u;  // north (nb4[3])
+      }
+    }
+    if (edge) atomicOr(&s_edge, edge);
+    __syncthreads();
+    if (tid < 5) {
+      const unsigned e = s_edge;
+      int ntx = tx, nty = ty;
+      bool want = false;
+      if (tid == 0) { want = (e & 1u) && ty > 0; nty = ty - 1; }
+      else if (tid == 1) { want = (e & 2u) && tx > 0; ntx = tx - 1; }
+      else if (tid == 2) { want = (e & 4u) && tx + 1 < a.ntx; ntx = tx + 1; }
+      else if (tid == 3) { want = (e & 8u) && ty + 1 < a.nty; nty = ty + 1; }
+      else { want = capped; }
+      if (want) {
+        const uint32_t nt = (uint32_t)nty * (uint32_t)a.ntx + (uint32_t)ntx;
+        if (atomicMax(&a.tile_epoch[nt], a.epoch) < a.epoch) {
+          const uint32_t pos = atomicAdd(a.count_out, 1u);
+          a.list_out[pos] = nt;
+        }
+      }
+      if (tid == 0) {
+        atomicAdd(&a.stats[kStatVisits], 1ull);
+        atomicAdd(&a.stats[kStatSweeps], (unsigned long long)sweeps);
+      }
+    }
+    __syncthreads();  // s_edge / sT reuse by the next tile
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic speed field; k = global row-major index.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ double u01(uint64_t seed, uint64_t k) {
+  return (double)(splitmix64(seed ^ k) >> 11) * 0x1.0p-53;
+}
+
+__global__ void k_synth(double* F, uint64_t ld, uint32_t nx, uint32_t ny, uint64_t row0,
+                        uint64_t seed, double frac, uint64_t oseed, int64_t gi, int64_t gj) {
+  const uint64_t n = (uint64_t)nx * ny;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+       k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = k / nx, cc = k % nx;
+    const uint64_t grow = row0 + r;
+    const uint64_t gk = grow * nx + cc;
+    double v = 1.0 + 4.0 * u01(seed, gk);
+    if (frac > 0.0 && u01(oseed, gk) < frac) {
+      const int64_t di = (int64_t)cc - gi, dj = (int64_t)grow - gj;
+      if (!(di >= -1 && di <= 1 && dj >= -1 && dj <= 1)) v = dinf();
+    }
+    F[r * ld + cc] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launch wrappers
+// ---------------------------------------------------------------------------
+hipError_t launch_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, int64_t row_hi,
+                           hipStream_t st) {
+  const uint64_t n = (uint64_t)(row_hi - row_lo) * nx;
+  uint64_t blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fill_inf, dim3((unsigned)blocks), dim3(256), 0, st, T, ld, nx, row_lo,
+                     row_hi);
+  return hipGetLastError();
+}
+
+hipError_t launch_seed(double* T, uint64_t ld, int64_t gi, int64_t gj, uint32_t* list,
+                       uint32_t* count, uint32_t* tile_epoch, uint32_t epoch, uint32_t tile,
+                       int set_goal, hipStream_t st) {
+  hipLaunchKernelGGL(k_seed, dim3(1), dim3(64), 0, st, T, ld, gi, gj, list, count, tile_epoch,
+                     epoch, tile, set_goal);
+  return hipGetLastError();
+}
+
+hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_fim_pass, dim3(blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth(double* F, uint64_t ld, uint32_t nx, uint32_t ny, uint64_t row0,
+                        uint64_t seed, double frac, uint64_t oseed, int64_t gi, int64_t gj,
+                        hipStream_t st) {
+  const uint64_t n = (uint64_t)nx * ny;
+  uint64_t blocks = (n + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_synth, dim3((unsigned)blocks), dim3(256), 0, st, F, ld, nx, ny, row0, seed,
+                     frac, oseed, gi, gj);
+  return hipGetLastError();
+}
+
+}  // namespace dymu

@@ -1,0 +1,206 @@
+// planner_capi.cpp -- extern "C" forwarding layer (include/dymu_planner.h)
+// over PathPlanning_lib::DyMuPathPlanner.  Exceptions never cross the ABI:
+// an engine failure becomes DYMU_ERR_NO_DEVICE / DYMU_ERR_HIP.
+#include <cstring>
+#include <exception>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "DyMu.hpp"
+#include "dymu_planner.h"
+
+using PathPlanning_lib::DyMuPathPlanner;
+
+struct dymu_planner {
+  DyMuPathPlanner pl;
+  dymu_planner(double a, double b, double c, PathPlanning_lib::repairingAproach r)
+      : pl(a, b, c, r) {}
+};
+
+namespace {
+
+base::Waypoint wp(double x, double y, double z, double h) {
+  base::Waypoint w;
+  w.position[0] = x;
+  w.position[1] = y;
+  w.position[2] = z;
+  w.heading = h;
+  return w;
+}
+
+int engine_error(const std::exception& e) {
+  const std::string m = e.what();
+  return m.find("cannot create") != std::string::npos ? DYMU_ERR_NO_DEVICE : DYMU_ERR_HIP;
+}
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return DYMU_ERR_NOMEM;
+  } catch (const std::exception& e) {
+    return engine_error(e);
+  }
+}
+
+std::vector<std::vector<double>> to_rows(const double* a, unsigned nx, unsigned ny) {
+  std::vector<std::vector<double>> m(ny, std::vector<double>(nx));
+  for (unsigned j = 0; j < ny; ++j) std::memcpy(m[j].data(), a + (size_t)j * nx, sizeof(double) * nx);
+  return m;
+}
+
+void from_rows(const std::vector<std::vector<double>>& m, double* out) {
+  size_t off = 0;
+  for (const auto& r : m) {
+    std::memcpy(out + off, r.data(), sizeof(double) * r.size());
+    off += r.size();
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int dymu_planner_create(dymu_planner** out, double risk_distance, double reconnect_distance,
+                        double risk_ratio, int approach) {
+  if (!out) return DYMU_ERR_ARG;
+  return guarded([&] {
+    *out = new dymu_planner(risk_distance, reconnect_distance, risk_ratio,
+                            approach == 1 ? PathPlanning_lib::SWEEPING
+                                          : PathPlanning_lib::CONSERVATIVE);
+    return DYMU_OK;
+  });
+}
+
+void dymu_planner_destroy(dymu_planner* p) { delete p; }
+
+int dymu_planner_set_engine_options(dymu_planner* p, const dymu_opts* o) {
+  if (!p || !o) return DYMU_ERR_ARG;
+  p->pl.setEngineOptions(*o);
+  return DYMU_OK;
+}
+
+int dymu_planner_init_global_layer(dymu_planner* p, double globalres, double localres,
+                                   uint32_t nx, uint32_t ny, double offx, double offy) {
+  if (!p || nx == 0 || ny == 0) return DYMU_ERR_ARG;
+  return guarded([&] { return (int)p->pl.initGlobalLayer(globalres, localres, nx, ny, {offx, offy}); });
+}
+
+int dymu_planner_set_cost_map(dymu_planner* p, const double* cost_map, uint32_t nx, uint32_t ny) {
+  if (!p || !cost_map) return DYMU_ERR_ARG;
+  return guarded([&] { return (int)p->pl.setCostMap(to_rows(cost_map, nx, ny)); });
+}
+
+int dymu_planner_compute_cost_map(dymu_planner* p, const double* lut, int lut_len,
+                                  const double* slopes, int n_slopes, const char* const* loc_modes,
+                                  int n_locs, const double* elevation, const double* terrain) {
+  if (!p || !lut || !slopes || !loc_modes || !elevation || !terrain || lut_len <= 0 ||
+      n_slopes <= 0 || n_locs <= 0)
+    return DYMU_ERR_ARG;
+  return guarded([&] {
+    std::vector<std::string> modes;
+    for (int k = 0; k < n_locs; ++k) modes.emplace_back(loc_modes[k] ? loc_modes[k] : "");
+    const unsigned nx = p->pl.sizeX(), ny = p->pl.sizeY();
+    return (int)p->pl.computeCostMap(std::vector<double>(lut, lut + lut_len),
+                                     std::vector<double>(slopes, slopes + n_slopes), modes,
+                                     to_rows(elevation, nx, ny), to_rows(terrain, nx, ny));
+  });
+}
+
+int dymu_planner_set_goal(dymu_planner* p, double x, double y, double z, double h) {
+  if (!p) return DYMU_ERR_ARG;
+  return guarded([&] { return (int)p->pl.setGoal(wp(x, y, z, h)); });
+}
+
+int dymu_planner_compute_total_cost_map(dymu_planner* p, double x, double y, double z, double h) {
+  if (!p) return DYMU_ERR_ARG;
+  return guarded([&] { return (int)p->pl.computeTotalCostMap(wp(x, y, z, h)); });
+}
+
+int dymu_planner_compute_entire_total_cost_map(dymu_planner* p) {
+  if (!p) return DYMU_ERR_ARG;
+  return guarded([&] { return (int)p->pl.computeEntireTotalCostMap(); });
+}
+
+int dymu_planner_get_total_cost_matrix(dymu_planner* p, double* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  return guarded([&] { from_rows(p->pl.getTotalCostMatrix(), out); return DYMU_OK; });
+}
+
+int dymu_planner_get_global_cost_matrix(dymu_planner* p, double* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  return guarded([&] { from_rows(p->pl.getGlobalCostMatrix(), out); return DYMU_OK; });
+}
+
+int dymu_planner_get_hazard_density_matrix(dymu_planner* p, double* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  return guarded([&] { from_rows(p->pl.getHazardDensityMatrix(), out); return DYMU_OK; });
+}
+
+int dymu_planner_get_trafficability_matrix(dymu_planner* p, double* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  return guarded([&] { from_rows(p->pl.getTrafficabilityMatrix(), out); return DYMU_OK; });
+}
+
+int dymu_planner_get_total_cost_raw(dymu_planner* p, double* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  const size_t n = (size_t)p->pl.sizeX() * p->pl.sizeY();
+  std::memcpy(out, p->pl.totalCostData(), sizeof(double) * n);
+  return DYMU_OK;
+}
+
+int dymu_planner_get_total_cost(dymu_planner* p, double x, double y, double z, double h,
+                                double* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  return guarded([&] { *out = p->pl.getTotalCost(wp(x, y, z, h)); return DYMU_OK; });
+}
+
+int dymu_planner_get_path(dymu_planner* p, double x, double y, double z, double h,
+                          double* out, int max_wp) {
+  if (!p || !out || max_wp < 0) return DYMU_ERR_ARG;
+  return guarded([&] {
+    const std::vector<base::Waypoint> path = p->pl.getPath(wp(x, y, z, h));
+    const int n = (int)path.size();
+    for (int k = 0; k < n && k < max_wp; ++k) {
+      out[4 * k + 0] = path[k].position[0];
+      out[4 * k + 1] = path[k].position[1];
+      out[4 * k + 2] = path[k].position[2];
+      out[4 * k + 3] = path[k].heading;
+    }
+    return n;
+  });
+}
+
+int dymu_planner_get_locomotion_mode(dymu_planner* p, double x, double y, double z, double h,
+                                     char* buf, int buflen) {
+  if (!p || !buf || buflen <= 0) return DYMU_ERR_ARG;
+  return guarded([&] {
+    const std::string m = p->pl.getLocomotionMode(wp(x, y, z, h));
+    std::strncpy(buf, m.c_str(), (size_t)buflen - 1);
+    buf[buflen - 1] = '\0';
+    return (int)m.size();
+  });
+}
+
+int dymu_planner_set_hazard_density(dymu_planner* p, const double* hd) {
+  if (!p || !hd) return DYMU_ERR_ARG;
+  const size_t n = (size_t)p->pl.sizeX() * p->pl.sizeY();
+  return guarded([&] { return (int)p->pl.setHazardDensity(std::vector<double>(hd, hd + n)); });
+}
+
+int dymu_planner_set_trafficability(dymu_planner* p, const double* tr) {
+  if (!p || !tr) return DYMU_ERR_ARG;
+  const size_t n = (size_t)p->pl.sizeX() * p->pl.sizeY();
+  return guarded([&] { return (int)p->pl.setTrafficability(std::vector<double>(tr, tr + n)); });
+}
+
+int dymu_planner_last_stats(dymu_planner* p, dymu_stats* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  *out = p->pl.lastStats();
+  return DYMU_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,215 @@
+"""dymu -- Python binding of the MI355X DyMu total-cost propagation engine.
+
+Thin ctypes layer over the two in-tree shared libraries:
+
+* ``lib/libdymu_fim.so``     -- HIP kernels + C-ABI (include/dymu_fim.h)
+* ``lib/libdymu_planner.so`` -- host C++ ``PathPlanning_lib::DyMuPathPlanner``
+                                (include/DyMu.hpp) behind include/dymu_planner.h
+
+There is no CPU fallback: if the HIP library is missing or no device is
+visible, every entry point raises ``DymuError``.  The CPU oracle under
+``oracle/`` is test infrastructure and is never imported from here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIBDIR = os.path.normpath(os.path.join(_HERE, "..", "lib"))
+
+DYMU_OK = 0
+_ERRS = {
+    -1: "invalid argument",
+    -2: "HIP runtime error",
+    -3: "device out of memory",
+    -4: "pass cap reached before convergence",
+    -5: "no HIP device",
+    -6: "RCCL error",
+    -7: "call out of sequence",
+}
+
+
+class DymuError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        super().__init__(f"dymu status {status} ({_ERRS.get(status, 'unknown')}) {what}".strip())
+
+
+class DymuOpts(ctypes.Structure):
+    _fields_ = [
+        ("device", ctypes.c_int),
+        ("passes_per_check", ctypes.c_int),
+        ("max_passes", ctypes.c_int),
+        ("max_inner", ctypes.c_int),
+        ("grid_blocks", ctypes.c_int),
+    ]
+
+
+class DymuStats(ctypes.Structure):
+    _fields_ = [
+        ("passes", ctypes.c_uint64),
+        ("launches", ctypes.c_uint64),
+        ("tile_visits", ctypes.c_uint64),
+        ("inner_sweeps", ctypes.c_uint64),
+        ("max_active", ctypes.c_uint64),
+        ("rounds", ctypes.c_uint64),
+        ("ms", ctypes.c_double),
+        ("tile_w", ctypes.c_int),
+        ("tile_h", ctypes.c_int),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_u32, _u64, _i32, _vp = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p
+
+# name -> (restype, argtypes)
+FIM_SYMBOLS = {
+    "dymu_create": (_i32, [ctypes.POINTER(_vp), ctypes.POINTER(DymuOpts)]),
+    "dymu_destroy": (_i32, [_vp]),
+    "dymu_solve": (_i32, [_vp, _dp, _u32, _u32, _u32, _u32, _dp, ctypes.POINTER(DymuStats)]),
+    "dymu_solve_device": (_i32, [_vp, _vp, _vp, _u32, _u32, _u64, _u32, _u32, _vp,
+                                 ctypes.POINTER(DymuStats)]),
+    "dymu_synth_speed": (_i32, [_vp, _vp, _u32, _u32, _u64, _u64, _u64, ctypes.c_double, _u64,
+                                _u32, _u32, _vp]),
+    "dymu_device_alloc": (_i32, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    "dymu_device_free": (_i32, [_vp, _vp]),
+    "dymu_memcpy_d2h": (_i32, [_vp, _vp, _vp, ctypes.c_size_t]),
+    "dymu_memcpy_h2d": (_i32, [_vp, _vp, _vp, ctypes.c_size_t]),
+    "dymu_set_profiling": (_i32, [_vp, _i32]),
+    "dymu_last_pass_timing": (_i32, [_vp, ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_uint64)]),
+    "dymu_strerror": (ctypes.c_char_p, [_i32]),
+    "dymu_last_error": (ctypes.c_char_p, [_vp]),
+    "dymu_abi_version": (_i32, []),
+    "dymu_device_count": (_i32, []),
+}
+
+_fim = None
+
+
+def lib_path(name: str) -> str:
+    return os.path.join(_LIBDIR, name)
+
+
+def load_fim() -> ctypes.CDLL:
+    """Load libdymu_fim.so (RTLD_GLOBAL so the planner library resolves it)."""
+    global _fim
+    if _fim is None:
+        path = lib_path("libdymu_fim.so")
+        if not os.path.exists(path):
+            raise DymuError(-5, f"HIP extension missing: {path} (run __graft_entry__.build())")
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in FIM_SYMBOLS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _fim = lib
+    return _fim
+
+
+def _check(rc: int, ctx=None):
+    if rc != DYMU_OK:
+        what = ""
+        if ctx is not None:
+            msg = load_fim().dymu_last_error(ctx)
+            what = msg.decode() if msg else ""
+        raise DymuError(rc, what)
+
+
+@dataclass
+class SolveResult:
+    T: np.ndarray
+    stats: dict
+
+
+class Engine:
+    """One HIP context (stream + workspace) on one device."""
+
+    def __init__(self, device: int = -1, passes_per_check: int = 0, max_passes: int = 0,
+                 max_inner: int = 0, grid_blocks: int = 0):
+        lib = load_fim()
+        self._lib = lib
+        opts = DymuOpts(device, passes_per_check, max_passes, max_inner, grid_blocks)
+        ctx = _vp()
+        rc = lib.dymu_create(ctypes.byref(ctx), ctypes.byref(opts))
+        if rc != DYMU_OK:
+            raise DymuError(rc, "dymu_create")
+        self.ctx = ctx
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self._lib.dymu_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- host-buffer solve (planner path) --
+    def solve(self, F: np.ndarray, goal_i: int, goal_j: int) -> SolveResult:
+        F = np.ascontiguousarray(F, dtype=np.float64)
+        if F.ndim != 2:
+            raise ValueError("F must be 2-D [ny, nx]")
+        ny, nx = F.shape
+        T = np.empty_like(F)
+        st = DymuStats()
+        _check(self._lib.dymu_solve(self.ctx, F, nx, ny, goal_i, goal_j, T, ctypes.byref(st)),
+               self.ctx)
+        return SolveResult(T, st.as_dict())
+
+    # -- device-resident solve --
+    def solve_device(self, dF: int, dT: int, nx: int, ny: int, ld: int, goal_i: int,
+                     goal_j: int, stream: int = 0) -> dict:
+        st = DymuStats()
+        _check(self._lib.dymu_solve_device(self.ctx, dF, dT, nx, ny, ld, goal_i, goal_j,
+                                           stream or None, ctypes.byref(st)), self.ctx)
+        return st.as_dict()
+
+    def synth_speed(self, dF: int, nx: int, ny: int, ld: int, row0: int = 0, seed: int = 1,
+                    obst_frac: float = 0.0, obst_seed: int = 3, goal_i: int = 0,
+                    goal_j: int = 0, stream: int = 0):
+        _check(self._lib.dymu_synth_speed(self.ctx, dF, nx, ny, ld, row0, seed, obst_frac,
+                                          obst_seed, goal_i, goal_j, stream or None), self.ctx)
+
+    def alloc(self, nbytes: int) -> int:
+        p = _vp()
+        _check(self._lib.dymu_device_alloc(self.ctx, nbytes, ctypes.byref(p)), self.ctx)
+        return p.value
+
+    def free(self, p: int):
+        _check(self._lib.dymu_device_free(self.ctx, p), self.ctx)
+
+    def d2h(self, dst: np.ndarray, src: int):
+        _check(self._lib.dymu_memcpy_d2h(self.ctx, dst.ctypes.data, src, dst.nbytes), self.ctx)
+
+    def h2d(self, dst: int, src: np.ndarray):
+        src = np.ascontiguousarray(src)
+        _check(self._lib.dymu_memcpy_h2d(self.ctx, dst, src.ctypes.data, src.nbytes), self.ctx)
+
+    def set_profiling(self, on: bool):
+        _check(self._lib.dymu_set_profiling(self.ctx, 1 if on else 0), self.ctx)
+
+    def last_pass_timing(self):
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        _check(self._lib.dymu_last_pass_timing(self.ctx, ctypes.byref(ms), ctypes.byref(n)),
+               self.ctx)
+        return ms.value, n.value
+
+
+def device_count() -> int:
+    return load_fim().dymu_device_count()

@@ -1,0 +1,114 @@
+"""GPU parity tests of the HIP block-FIM engine through the C-ABI
+(libdymu_fim.so: dymu_solve / dymu_solve_device) against the CPU oracle.
+
+Tolerance: identical +inf mask and
+|T_gpu - T_ref| <= 1e-12 * max(1, T_ref).  The reference FMM and the FIM fixed
+point differ only at ulp level (measured <= 2.2e-15 relative)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-12
+
+
+def assert_parity(T, Tref):
+    inf_g, inf_r = np.isinf(T), np.isinf(Tref)
+    assert np.array_equal(inf_g, inf_r), f"inf mask differs at {np.argwhere(inf_g != inf_r)[:5]}"
+    fin = ~inf_r
+    err = np.abs(T[fin] - Tref[fin]) / np.maximum(1.0, Tref[fin])
+    assert err.max(initial=0.0) <= RTOL, f"max rel err {err.max()}"
+    return err.max(initial=0.0)
+
+
+def test_kat_mt19937_256(engine, oracle):
+    """SURVEY s8(c) KAT: reference sum(getTotalCostMatrix)=1.7066083890e+07,
+    T[1][1]=479.2433625750 at N=256."""
+    N = 256
+    F = oracle.mt_uniform(N * N).reshape(N, N)
+    r = engine.solve(F, N // 2, N // 2)
+    M = np.where(np.isinf(r.T), -1.0, r.T)
+    assert f"{M.sum():.10e}" == "1.7066083890e+07"
+    assert f"{r.T[1, 1]:.10f}" == "479.2433625750"
+    Tref, _ = oracle.fmm(F, (N // 2, N // 2))
+    assert_parity(r.T, Tref)
+
+
+@pytest.mark.parametrize("N", [512, 1024])
+def test_kat_mt19937(engine, oracle, N):
+    kat = {512: ("1.3467278246e+08", "972.7322452271"),
+           1024: ("1.0666255888e+09", "1913.6136177798")}[N]
+    F = oracle.mt_uniform(N * N).reshape(N, N)
+    r = engine.solve(F, N // 2, N // 2)
+    M = np.where(np.isinf(r.T), -1.0, r.T)
+    assert f"{M.sum():.10e}" == kat[0]
+    assert f"{r.T[1, 1]:.10f}" == kat[1]
+
+
+@pytest.mark.parametrize("nx,ny,frac,goal", [
+    (64, 64, 0.0, (32, 32)),
+    (128, 96, 0.02, (10, 80)),
+    (33, 65, 0.05, (1, 1)),          # ragged tiles, goal near the corner
+    (1, 1, 0.0, (0, 0)),             # single cell
+    (1, 300, 0.0, (0, 150)),         # one column
+    (300, 1, 0.0, (299, 0)),         # one row
+    (257, 129, 0.10, (128, 64)),
+    (500, 700, 0.25, (250, 350)),    # dense obstacles, disconnected pockets
+])
+def test_parity_random(engine, oracle, nx, ny, frac, goal):
+    F = oracle.synth_speed(nx, ny, seed=7, obst_frac=frac, obst_seed=11, goal=goal)
+    r = engine.solve(F, goal[0], goal[1])
+    Tref, _ = oracle.fmm(F, goal)
+    assert_parity(r.T, Tref)
+    assert r.T[goal[1], goal[0]] == 0.0
+
+
+def test_constant_speed_closed_form(engine):
+    """C=1: T on the axes equals the distance, T(+-1,+-1) = 1 + sqrt(2)/2 (:533)."""
+    N = 65
+    F = np.ones((N, N))
+    r = engine.solve(F, 32, 32)
+    T = r.T
+    for k in range(1, 20):
+        assert T[32, 32 + k] == float(k) and T[32 - k, 32] == float(k)
+    v = 1.0 + np.sqrt(2.0) / 2.0
+    for dj, di in ((1, 1), (-1, 1), (1, -1), (-1, -1)):
+        assert T[32 + dj, 32 + di] == v
+
+
+def test_device_resident_and_synth(engine, oracle):
+    """dymu_synth_speed on device == host generator; dymu_solve_device == oracle."""
+    nx, ny, g = 384, 320, (200, 100)
+    n = nx * ny
+    dF = engine.alloc(8 * n)
+    dT = engine.alloc(8 * n)
+    try:
+        engine.synth_speed(dF, nx, ny, nx, 0, 1, 0.02, 3, g[0], g[1])
+        Fd = np.empty((ny, nx))
+        engine.d2h(Fd, dF)
+        Fh = oracle.synth_speed(nx, ny, seed=1, obst_frac=0.02, obst_seed=3, goal=g)
+        assert np.array_equal(Fd, Fh)
+        st = engine.solve_device(dF, dT, nx, ny, nx, g[0], g[1])
+        T = np.empty((ny, nx))
+        engine.d2h(T, dT)
+        Tref, _ = oracle.fmm(Fh, g)
+        assert_parity(T, Tref)
+        assert st["passes"] > 0 and st["tile_visits"] >= st["passes"]
+    finally:
+        engine.free(dF)
+        engine.free(dT)
+
+
+def test_repeat_solves_reuse_context(engine, oracle):
+    """Epoch-stamped tile flags survive across solves of different sizes."""
+    for (nx, ny, g) in [(200, 200, (100, 100)), (64, 300, (3, 5)), (200, 200, (20, 180))]:
+        F = oracle.synth_speed(nx, ny, seed=5, obst_frac=0.03, obst_seed=9, goal=g)
+        r = engine.solve(F, g[0], g[1])
+        Tref, _ = oracle.fmm(F, g)
+        assert_parity(r.T, Tref)
+
+
+def test_bad_args(engine, dymu):
+    F = np.ones((8, 8))
+    with pytest.raises(dymu.DymuError):
+        engine.solve(F, 8, 0)
