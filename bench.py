@@ -1,0 +1,173 @@
+"""bench.py -- global total-cost-map propagation throughput (Mcells/s).
+
+Workload (BASELINE.json configs[2]): a 16384^2 synthetic grid, one goal at the
+centre, F = 1 + 4*u(splitmix64) with 2% iid obstacles,
+generated in HBM.  One "step" = one full solve (computeEntireTotalCostMap's
+propagation: T initialised, relaxed to convergence, result in HBM).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--size S] [--obst P]
+
+N > 1 runs under torch.distributed.run, one rank per GPU: the grid is cut in
+row slabs, one per rank, with RCCL halo exchange (dymu_sharded_*); value is
+the whole-job rate N^2 / max-over-ranks solve time.
+
+Rank 0 prints ONE JSON line with the roofline of the dominant kernel
+(k_fim_pass, per-launch HIP events over the timed region) and the CPU baseline
+(the oracle's heap FMM, same pop order as the reference, one thread, on a
+bounded sample).
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "planning-path_planning_amd"))
+
+import numpy as np  # noqa: E402
+
+import dymu  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
+BYTES_PER_CELL_VISIT = 24  # read T 8 + read F 8 + write T 8
+BYTES_PER_CELL_SOLVE = 16  # read F once + write T once
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--size", type=int, default=16384)
+    ap.add_argument("--obst", type=float, default=0.02)
+    ap.add_argument("--cpu-sample", type=int, default=8192,
+                    help="edge of the grid the CPU baseline solves (0 = skip)")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="no per-launch events (roofline reported as null)")
+    return ap.parse_args()
+
+
+def cpu_baseline(n_edge, obst):
+    """Oracle heap FMM (reference pop order) on an n_edge^2 config-3 grid, 1 thread."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi
+
+    o = oracle_ffi.load()
+    g = (n_edge // 2, n_edge // 2)
+    F = o.synth_speed(n_edge, n_edge, seed=1, obst_frac=obst, obst_seed=3, goal=g)
+    t0 = time.perf_counter()
+    T, _ = o.fmm(F, g)
+    dt = time.perf_counter() - t0
+    return {
+        "value": n_edge * n_edge / dt / 1e6,
+        "unit": "Mcells/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{n_edge}x{n_edge} config-3 grid (2% obstacles, goal centre), oracle heap "
+                  f"FMM with the reference's pop order, 1 thread, {dt:.1f}s; "
+                  f"host {platform.processor() or platform.machine()}",
+    }
+
+
+def run_single(args):
+    N = args.size
+    eng = dymu.Engine(device=int(os.environ.get("LOCAL_RANK", "0")))
+    n = N * N
+    dF, dT = eng.alloc(8 * n), eng.alloc(8 * n)
+    g = (N // 2, N // 2)
+    eng.synth_speed(dF, N, N, N, 0, 1, args.obst, 3, g[0], g[1])
+    for _ in range(args.warmup):
+        eng.solve_device(dF, dT, N, N, N, g[0], g[1])
+    prof = not args.no_profile
+    eng.set_profiling(prof)
+    tot = {"passes": 0, "tile_visits": 0, "inner_sweeps": 0, "launches": 0}
+    kern_ms, kern_n = 0.0, 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = eng.solve_device(dF, dT, N, N, N, g[0], g[1])
+        for k in tot:
+            tot[k] += st[k]
+        if prof:
+            ms, nl = eng.last_pass_timing()
+            kern_ms += ms
+            kern_n += nl
+    dt = time.perf_counter() - t0
+    eng.set_profiling(False)
+    T = np.empty(2)
+    eng.d2h(T, dT)  # touch the result
+    eng.free(dF)
+    eng.free(dT)
+    eng.close()
+    return dt, tot, kern_ms, kern_n, st
+
+
+def main():
+    args = parse()
+    world = args.gpus
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        import bench_sharded
+
+        res = bench_sharded.run(args)
+        if res is None:
+            return
+        dt, tot, kern_ms, kern_n, st = res
+    else:
+        dt, tot, kern_ms, kern_n, st = run_single(args)
+    if rank != 0:
+        return
+    N = args.size
+    K = args.steps
+    value = N * N * K / dt / 1e6
+    roof = None
+    if kern_n > 0 and kern_ms > 0:
+        cells_visited = tot["tile_visits"] * st["tile_w"] * st["tile_h"]
+        bytes_alg = cells_visited * BYTES_PER_CELL_VISIT
+        achieved = bytes_alg / (kern_ms * 1e-3) / 1e9
+        roof = {
+            "bound": "hbm",
+            "achieved": round(achieved, 3),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 6),
+            "traffic": None,
+            "kernel": "k_fim_pass",
+            "bytes_per_launch": bytes_alg / kern_n,
+            "avg_launch_us": kern_ms * 1e3 / kern_n,
+            "per_unit": "24 B per cell-visit (SURVEY s8(d)(ii))",
+            "headline_solve_GBs": round(N * N * BYTES_PER_CELL_SOLVE * K / dt / 1e9, 3),
+        }
+    line = {
+        "metric": "global total-cost-map Mcells/s (16384^2 grid); iters to converge",
+        "value": round(value, 3),
+        "unit": "Mcells/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / K * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": f"config 3: {N}x{N} grid, {world}x MI355X, splitmix64 U(1,5) speed, "
+                        f"{args.obst:.0%} iid obstacles, goal centre, full solve",
+            "grid": N,
+            "parallelism": "single" if world == 1 else f"row-slab x{world}",
+            "passes_per_solve": tot["passes"] / K,
+            "tile_visits_per_solve": tot["tile_visits"] / K,
+            "inner_sweeps_per_solve": tot["inner_sweeps"] / K,
+        },
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if world == 1 and args.cpu_sample > 0:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.obst)
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

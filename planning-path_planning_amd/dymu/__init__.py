@@ -213,3 +213,176 @@ class Engine:
 
 def device_count() -> int:
     return load_fim().dymu_device_count()
+
+
+# ---------------------------------------------------------------------------
+# host planner: PathPlanning_lib::DyMuPathPlanner behind include/dymu_planner.h
+# ---------------------------------------------------------------------------
+_d = ctypes.c_double
+PLANNER_SYMBOLS = {
+    "dymu_planner_create": (_i32, [ctypes.POINTER(_vp), _d, _d, _d, _i32]),
+    "dymu_planner_destroy": (None, [_vp]),
+    "dymu_planner_set_engine_options": (_i32, [_vp, ctypes.POINTER(DymuOpts)]),
+    "dymu_planner_init_global_layer": (_i32, [_vp, _d, _d, _u32, _u32, _d, _d]),
+    "dymu_planner_set_cost_map": (_i32, [_vp, _dp, _u32, _u32]),
+    "dymu_planner_compute_cost_map": (_i32, [_vp, _dp, _i32, _dp, _i32,
+                                             ctypes.POINTER(ctypes.c_char_p), _i32, _dp, _dp]),
+    "dymu_planner_set_goal": (_i32, [_vp, _d, _d, _d, _d]),
+    "dymu_planner_compute_total_cost_map": (_i32, [_vp, _d, _d, _d, _d]),
+    "dymu_planner_compute_entire_total_cost_map": (_i32, [_vp]),
+    "dymu_planner_get_total_cost_matrix": (_i32, [_vp, _dp]),
+    "dymu_planner_get_global_cost_matrix": (_i32, [_vp, _dp]),
+    "dymu_planner_get_hazard_density_matrix": (_i32, [_vp, _dp]),
+    "dymu_planner_get_trafficability_matrix": (_i32, [_vp, _dp]),
+    "dymu_planner_get_total_cost_raw": (_i32, [_vp, _dp]),
+    "dymu_planner_get_total_cost": (_i32, [_vp, _d, _d, _d, _d, ctypes.POINTER(_d)]),
+    "dymu_planner_get_path": (_i32, [_vp, _d, _d, _d, _d, _dp, _i32]),
+    "dymu_planner_get_locomotion_mode": (_i32, [_vp, _d, _d, _d, _d, ctypes.c_char_p, _i32]),
+    "dymu_planner_set_hazard_density": (_i32, [_vp, _dp]),
+    "dymu_planner_set_trafficability": (_i32, [_vp, _dp]),
+    "dymu_planner_last_stats": (_i32, [_vp, ctypes.POINTER(DymuStats)]),
+}
+
+_pl = None
+
+
+def load_planner() -> ctypes.CDLL:
+    global _pl
+    if _pl is None:
+        load_fim()
+        path = lib_path("libdymu_planner.so")
+        if not os.path.exists(path):
+            raise DymuError(-5, f"planner library missing: {path} (run __graft_entry__.build())")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in PLANNER_SYMBOLS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _pl = lib
+    return _pl
+
+
+def _b(rc: int) -> bool:
+    if rc < 0:
+        raise DymuError(rc)
+    return bool(rc)
+
+
+class Planner:
+    """Python mirror of PathPlanning_lib::DyMuPathPlanner (reference
+    src/DyMu.hpp:397-609, global layer).  Method names follow the reference;
+    waypoints are (x, y[, z, heading]) tuples; grids are numpy [ny, nx]."""
+
+    CONSERVATIVE, SWEEPING = 0, 1
+
+    def __init__(self, risk_distance=1.0, reconnect_distance=1.0, risk_ratio=1.0,
+                 approach=CONSERVATIVE, device: int = -1):
+        self._lib = load_planner()
+        h = _vp()
+        rc = self._lib.dymu_planner_create(ctypes.byref(h), risk_distance, reconnect_distance,
+                                           risk_ratio, approach)
+        if rc != DYMU_OK:
+            raise DymuError(rc, "dymu_planner_create")
+        self.h = h
+        self.nx = self.ny = 0
+        if device >= 0:
+            o = DymuOpts(device, 0, 0, 0, 0)
+            _check(self._lib.dymu_planner_set_engine_options(self.h, ctypes.byref(o)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._lib.dymu_planner_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _wp(w):
+        w = tuple(w) + (0.0,) * (4 - len(w))
+        return float(w[0]), float(w[1]), float(w[2]), float(w[3])
+
+    def _grid(self, a):
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        if a.shape != (self.ny, self.nx):
+            raise ValueError(f"expected [{self.ny}, {self.nx}] grid, got {a.shape}")
+        return a
+
+    def initGlobalLayer(self, globalres, localres, nx, ny, offset=(0.0, 0.0)) -> bool:
+        self.nx, self.ny = int(nx), int(ny)
+        return _b(self._lib.dymu_planner_init_global_layer(self.h, globalres, localres, nx, ny,
+                                                           offset[0], offset[1]))
+
+    def setCostMap(self, cost_map) -> bool:
+        a = np.ascontiguousarray(cost_map, dtype=np.float64)
+        ny, nx = a.shape
+        return _b(self._lib.dymu_planner_set_cost_map(self.h, a, nx, ny))
+
+    def computeCostMap(self, cost_data, slope_values, locomotion_modes, elevation,
+                       terrain_map) -> bool:
+        lut = np.ascontiguousarray(cost_data, dtype=np.float64)
+        sl = np.ascontiguousarray(slope_values, dtype=np.float64)
+        modes = (ctypes.c_char_p * len(locomotion_modes))(*[m.encode() for m in locomotion_modes])
+        return _b(self._lib.dymu_planner_compute_cost_map(
+            self.h, lut, len(lut), sl, len(sl), modes, len(locomotion_modes),
+            self._grid(elevation), self._grid(terrain_map)))
+
+    def setGoal(self, w) -> bool:
+        return _b(self._lib.dymu_planner_set_goal(self.h, *self._wp(w)))
+
+    def computeTotalCostMap(self, w) -> bool:
+        return _b(self._lib.dymu_planner_compute_total_cost_map(self.h, *self._wp(w)))
+
+    def computeEntireTotalCostMap(self) -> bool:
+        return _b(self._lib.dymu_planner_compute_entire_total_cost_map(self.h))
+
+    def _matrix(self, fn):
+        out = np.empty((self.ny, self.nx))
+        _check(fn(self.h, out))
+        return out
+
+    def getTotalCostMatrix(self):
+        return self._matrix(self._lib.dymu_planner_get_total_cost_matrix)
+
+    def getGlobalCostMatrix(self):
+        return self._matrix(self._lib.dymu_planner_get_global_cost_matrix)
+
+    def getHazardDensityMatrix(self):
+        return self._matrix(self._lib.dymu_planner_get_hazard_density_matrix)
+
+    def getTrafficabilityMatrix(self):
+        return self._matrix(self._lib.dymu_planner_get_trafficability_matrix)
+
+    def totalCostRaw(self):
+        return self._matrix(self._lib.dymu_planner_get_total_cost_raw)
+
+    def getTotalCost(self, w) -> float:
+        out = ctypes.c_double()
+        _check(self._lib.dymu_planner_get_total_cost(self.h, *self._wp(w), ctypes.byref(out)))
+        return out.value
+
+    def getPath(self, w, max_wp: int = 1 << 20) -> np.ndarray:
+        buf = np.empty(4 * max_wp)
+        n = self._lib.dymu_planner_get_path(self.h, *self._wp(w), buf, max_wp)
+        if n < 0:
+            raise DymuError(n)
+        return buf[:4 * min(n, max_wp)].reshape(-1, 4).copy()
+
+    def getLocomotionMode(self, w) -> str:
+        buf = ctypes.create_string_buffer(256)
+        _check(min(0, self._lib.dymu_planner_get_locomotion_mode(self.h, *self._wp(w), buf, 256)))
+        return buf.value.decode()
+
+    def setHazardDensity(self, hd) -> bool:
+        return _b(self._lib.dymu_planner_set_hazard_density(self.h, self._grid(hd)))
+
+    def setTrafficability(self, tr) -> bool:
+        return _b(self._lib.dymu_planner_set_trafficability(self.h, self._grid(tr)))
+
+    def lastStats(self) -> dict:
+        st = DymuStats()
+        _check(self._lib.dymu_planner_last_stats(self.h, ctypes.byref(st)))
+        return st.as_dict()

@@ -1,0 +1,181 @@
+"""CPU tests of the oracle (the checker): pinned to the reference-run KATs of
+SURVEY.md s8(c), closed forms, and the committed golden fixtures."""
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+INF = np.inf
+
+
+def gold(name):
+    return np.load(os.path.join(GOLD, name + ".npy"), allow_pickle=False)
+
+
+# reference computeEntireTotalCostMap on mt19937_64(1) U(1,5)
+# costs, goal (N/2, N/2): (sum of getTotalCostMatrix, T[1][1]).
+KAT = {
+    256: ("1.7066083890e+07", "479.2433625750"),
+    512: ("1.3467278246e+08", "972.7322452271"),
+    1024: ("1.0666255888e+09", "1913.6136177798"),
+}
+
+
+@pytest.mark.parametrize("N", sorted(KAT))
+def test_kat_reference_checksums(oracle, N):
+    F = oracle.mt_uniform(N * N).reshape(N, N)
+    T, rc = oracle.fmm(F, (N // 2, N // 2))
+    M = np.where(np.isinf(T), -1.0, T)
+    assert f"{M.sum():.10e}" == KAT[N][0]
+    assert f"{T[1, 1]:.10f}" == KAT[N][1]
+
+
+@pytest.mark.parametrize("N,frac", [(64, 0.0), (96, 0.05), (128, 0.2)])
+def test_heap_equals_linear_bitwise(oracle, N, frac):
+    """The heap band with key (T, first-insertion seq) pops in exactly the
+    order of minCostGlobalNode's linear scan (:551-568)."""
+    F = oracle.synth_speed(N, N, seed=3, obst_frac=frac, obst_seed=4, goal=(N // 3, N // 2))
+    T1, r1 = oracle.fmm(F, (N // 3, N // 2), linear=True)
+    T2, r2 = oracle.fmm(F, (N // 3, N // 2), linear=False)
+    assert np.array_equal(T1, T2) and r1 == r2
+
+
+def test_early_exit_heap_equals_linear(oracle):
+    N = 80
+    F = oracle.synth_speed(N, N, seed=9, obst_frac=0.05, obst_seed=2, goal=(40, 40))
+    F[14:17, 9:12] = 2.0  # isSafeNode: start and its 8 neighbours free (:410-422)
+    T1, r1, c1 = oracle.fmm(F, (40, 40), start=(10, 15), linear=True, want_closed=True)
+    T2, r2, c2 = oracle.fmm(F, (40, 40), start=(10, 15), linear=False, want_closed=True)
+    assert np.array_equal(T1, T2) and np.array_equal(c1, c2) and r1 == r2 == 1
+    assert c1[15, 10] and c1[14, 10] and c1[16, 10] and c1[15, 9] and c1[15, 11]
+
+
+def test_eikonal_update_cases(oracle):
+    """:531-535 branches."""
+    s2 = np.sqrt(2.0)
+    assert oracle.eikonal(0.0, 0.0, 1.0) == (0.0 + 0.0 + np.sqrt(2.0)) / 2
+    assert oracle.eikonal(INF, 3.0, 2.0) == 5.0
+    assert oracle.eikonal(3.0, INF, 2.0) == 5.0
+    assert oracle.eikonal(1.0, 4.0, 2.0) == 3.0       # |Tx-Ty| >= C: one-sided
+    assert oracle.eikonal(INF, INF, 1.0) == INF
+    v = oracle.eikonal(1.0, 1.5, 1.0)
+    assert v == (1.0 + 1.5 + np.sqrt(2 * 1.0 - 0.25)) / 2
+    assert oracle.eikonal(0.0, 0.0, s2) == np.sqrt(4.0) / 2
+
+
+def test_closed_form_constant_speed(oracle):
+    N = 65
+    T, _ = oracle.fmm(np.ones((N, N)), (32, 32))
+    for k in range(1, 30):
+        assert T[32, 32 + k] == k and T[32, 32 - k] == k and T[32 + k, 32] == k
+    assert T[33, 33] == 1 + np.sqrt(2) / 2
+
+
+def test_jacobi_fixed_point_matches_fmm(oracle):
+    """the FMM output is the Jacobi fixed point up to ulps."""
+    N = 96
+    F = oracle.synth_speed(N, N, seed=1, obst_frac=0.02, obst_seed=3, goal=(48, 48))
+    Tf, _ = oracle.fmm(F, (48, 48))
+    Tj, sweeps = oracle.jacobi(F, (48, 48))
+    assert np.array_equal(np.isinf(Tf), np.isinf(Tj))
+    fin = np.isfinite(Tf)
+    rel = np.abs(Tf[fin] - Tj[fin]) / np.maximum(1, Tf[fin])
+    assert rel.max() < 1e-13
+    r, cnt = oracle.residual(F, Tj, (48, 48))
+    assert cnt == 0 and r == 0.0
+
+
+def test_unreachable_and_obstacles_stay_inf(oracle):
+    N = 40
+    F = np.ones((N, N))
+    F[:, 20] = INF                      # wall
+    T, rc = oracle.fmm(F, (5, 5))
+    assert np.isinf(T[:, 20]).all() and np.isinf(T[:, 21:]).all()
+    assert np.isfinite(T[:, :20]).all() and rc == 0
+
+
+def test_golden_setcost(oracle):
+    cost = gold("setcost64_cost")
+    g = tuple(int(x) for x in gold("setcost64_goal"))
+    N = cost.shape[0]
+    st = oracle.new_state(N, N)
+    oracle.lib.oracle_set_cost_map(cost.ravel(), cost.size, st["cost"].ravel(),
+                                   st["is_obstacle"].ravel(), st["traff"].ravel(),
+                                   st["hazard"].ravel())
+    F = oracle.pack_speed(st["cost"], st["hazard"], st["traff"], st["is_obstacle"])
+    T, _ = oracle.fmm(F, g)
+    assert np.array_equal(T, gold("setcost64_T"))
+
+
+def test_golden_terrain(oracle):
+    from gen_golden import terrain_inputs
+    elev, terr, lut, slopes = terrain_inputs(128)
+    assert np.array_equal(elev, gold("terrain128_elev"))
+    st = oracle.new_state(128, 128)
+    oracle.compute_cost_map(st, 0.5, lut, slopes, 1, elev, terr)
+    assert np.array_equal(st["cost"], gold("terrain128_cost"))
+    F = oracle.pack_speed(st["cost"], st["hazard"], st["traff"], st["is_obstacle"], res=0.5)
+    T, _ = oracle.fmm(F, tuple(int(x) for x in gold("terrain128_goal")))
+    assert np.array_equal(T, gold("terrain128_T"))
+    # borders are forced to obstacles by computeCostMap (:162-163)
+    assert np.isinf(T[0, :]).all() and np.isinf(T[:, 0]).all()
+
+
+def test_cost_map_q1_carry_over(oracle):
+    """Q1: a second computeCostMap compounds the previous smoothed cost."""
+    from gen_golden import terrain_inputs
+    elev, terr, lut, slopes = terrain_inputs(32)
+    st = oracle.new_state(32, 32)
+    oracle.compute_cost_map(st, 1.0, lut, slopes, 1, elev, terr)
+    c1 = st["cost"].copy()
+    oracle.compute_cost_map(st, 1.0, lut, slopes, 1, elev, terr)
+    assert not np.array_equal(c1, st["cost"])
+    i, j = 10, 10
+    rc = st["raw_cost"]
+    expect = (c1[j, i] + rc[j - 1, i] + rc[j, i - 1] + rc[j, i + 1] + rc[j + 1, i]) / 5
+    assert st["cost"][j, i] == expect
+
+
+def test_cost_map_multi_locomotion_q2(oracle):
+    """Q2: with several modes, mode 0 is skipped (loop starts at i=1)."""
+    N = 16
+    elev = np.zeros((N, N))
+    terr = np.ones((N, N))
+    # 2 terrains x 2 modes x 2 slopes; mode 0 cheapest but ignored
+    lut = np.array([9, 9, 9, 9,  1, 1, 3, 3], dtype=np.float64)
+    st = oracle.new_state(N, N)
+    oracle.compute_cost_map(st, 1.0, lut, np.array([0.0, 30.0]), 2, elev, terr)
+    assert st["raw_cost"][5, 5] == 3.0 and st["loc_mode"][5, 5] == 1
+
+
+def test_set_goal_validation(oracle):
+    obs = np.zeros((10, 10), dtype=np.uint8)
+    obs[5, 6] = 1
+    assert oracle.set_goal(10, 10, 1.0, (0, 0), (3.2, 3.6), obs) == (3, 4)
+    assert oracle.set_goal(10, 10, 1.0, (0, 0), (5.0, 5.0), obs) is None   # nb obstacle
+    assert oracle.set_goal(10, 10, 1.0, (0, 0), (0.2, 5.0), obs) is None   # border
+    assert oracle.set_goal(10, 10, 1.0, (0, 0), (-0.1, 5.0), obs) is None  # negative
+    assert oracle.set_goal(10, 10, 0.5, (1, 1), (3.0, 3.0), obs) == (4, 4)
+
+
+def test_early_exit_golden(oracle):
+    cost = gold("setcost64_cost")
+    g = tuple(int(x) for x in gold("setcost64_goal"))
+    F = np.where(cost <= 0, INF, cost)  # hazard 1 / traff 0 only matter for obstacles
+    T, rc, closed = oracle.fmm(F, g, start=(12, 50), linear=False, want_closed=True)
+    assert np.array_equal(T, gold("early64_T"))
+    assert np.array_equal(closed, gold("early64_closed"))
+    assert rc == int(gold("early64_rc")[0])
+
+
+def test_path_extraction_straight_line(oracle):
+    """Constant speed, goal on the start's row: gradient descent walks the row."""
+    N = 64
+    T, _ = oracle.fmm(np.ones((N, N)), (40, 32))
+    n, wp = oracle.global_path(T, (40, 32), res=1.0, start=(20.0, 32.0, 0.0), risk_distance=1.0)
+    assert n > 10
+    assert np.allclose(wp[:-1, 1], 32.0)
+    assert wp[-1, 0] == 40.0 and wp[-1, 1] == 32.0
+    steps = np.diff(wp[:-1, 0])
+    assert np.allclose(steps, 0.4)
