@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -28,10 +29,12 @@ struct dymu_ctx {
   dymu_opts opts{};
   int cu_count = 256;
 
+  int variant = 2;  // 1: 32x32 tile per workgroup, 2: 8x8 tile per wave (DYMU_KERNEL)
+
   // tile workspace
   uint32_t tiles_cap = 0;
-  uint32_t* d_lists = nullptr;       // 3 * tiles_cap
-  uint32_t* d_counts = nullptr;      // 4 words (3 used), own 16-byte block
+  uint32_t* d_lists = nullptr;       // 3 lists x kShards shards x tiles_cap
+  uint32_t* d_counts = nullptr;      // 3 x kShards words, own block
   uint32_t* d_tile_epoch = nullptr;  // tiles_cap
   unsigned long long* d_stats = nullptr;  // kStatSlots
   uint32_t epoch_base = 0;
@@ -75,7 +78,7 @@ int ensure_tiles(dymu_ctx* c, uint32_t ntiles) {
   c->d_lists = nullptr;
   c->d_tile_epoch = nullptr;
   c->tiles_cap = 0;
-  HIPC(c, hipMalloc(&c->d_lists, sizeof(uint32_t) * 3ull * ntiles));
+  HIPC(c, hipMalloc(&c->d_lists, sizeof(uint32_t) * 3ull * kShards * ntiles));
   HIPC(c, hipMalloc(&c->d_tile_epoch, sizeof(uint32_t) * (uint64_t)ntiles));
   HIPC(c, hipMemsetAsync(c->d_tile_epoch, 0, sizeof(uint32_t) * (uint64_t)ntiles, c->stream));
   c->tiles_cap = ntiles;
@@ -95,13 +98,14 @@ int ensure_cells(dymu_ctx* c, uint64_t cells) {
   return DYMU_OK;
 }
 
-uint32_t tiles_x(uint64_t nx) { return (uint32_t)((nx + kTileW - 1) / kTileW); }
-uint32_t tiles_y(uint64_t ny) { return (uint32_t)((ny + kTileH - 1) / kTileH); }
+int tile_w(const dymu_ctx* c) { return c->variant == 1 ? kTileW : kWaveTile; }
+int tile_h(const dymu_ctx* c) { return c->variant == 1 ? kTileH : kWaveTile; }
 
 int solve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
                uint32_t gi, uint32_t gj, hipStream_t st, dymu_stats* stats) {
   if (!dF || !dT || nx == 0 || ny == 0 || ld < nx || gi >= nx || gj >= ny) return DYMU_ERR_ARG;
-  const uint32_t ntx = tiles_x(nx), nty = tiles_y(ny);
+  const int TWd = tile_w(c), THd = tile_h(c);
+  const uint32_t ntx = (uint32_t)((nx + TWd - 1) / TWd), nty = (uint32_t)((ny + THd - 1) / THd);
   const uint64_t ntiles64 = (uint64_t)ntx * nty;
   if (ntiles64 >= (1ull << 31)) return DYMU_ERR_ARG;
   const uint32_t ntiles = (uint32_t)ntiles64;
@@ -115,12 +119,13 @@ int solve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t 
     c->epoch_base = 0;
   }
   const uint32_t eb = c->epoch_base;
-  uint32_t* lists[3] = {c->d_lists, c->d_lists + ntiles, c->d_lists + 2ull * ntiles};
-  uint32_t* counts[3] = {c->d_counts, c->d_counts + 1, c->d_counts + 2};
-  HIPC(c, hipMemsetAsync(c->d_counts, 0, 16, st));
-  HIPC(c, hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * kStatSlots, st));
+  const uint64_t lstride = (uint64_t)kShards * ntiles;
+  uint32_t* lists[3] = {c->d_lists, c->d_lists + lstride, c->d_lists + 2 * lstride};
+  uint32_t* counts[3] = {c->d_counts, c->d_counts + kShards, c->d_counts + 2 * kShards};
+  HIPC(c, hipMemsetAsync(c->d_counts, 0, sizeof(uint32_t) * 3 * kShards, st));
+  HIPC(c, hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * kShards * kStatSlots, st));
   HIPC(c, launch_fill_inf(dT, ld, nx, 0, ny, st));
-  const uint32_t gtile = (gj / kTileH) * ntx + (gi / kTileW);
+  const uint32_t gtile = (gj / THd) * ntx + (gi / TWd);
   HIPC(c, launch_seed(dT, ld, gi, gj, lists[0], counts[0], c->d_tile_epoch, eb + 1, gtile, 1, st));
 
   PassArgs a{};
@@ -133,7 +138,8 @@ int solve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t 
   a.nty = (int)nty;
   a.ghost_lo = 0;
   a.ghost_hi = 0;
-  a.max_inner = c->opts.max_inner > 0 ? c->opts.max_inner : 4 * (kTileW + kTileH);
+  a.max_inner = c->opts.max_inner > 0 ? c->opts.max_inner : 4 * (TWd + THd);
+  a.shard_cap = ntiles;
   a.tile_epoch = c->d_tile_epoch;
   a.stats = c->d_stats;
   const int blocks = c->opts.grid_blocks > 0 ? c->opts.grid_blocks : c->cu_count * 8;
@@ -159,16 +165,19 @@ int solve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t 
         }
         HIPC(c, hipEventRecord(c->prof_ev[prof_used], st));
       }
-      HIPC(c, launch_pass(a, blocks, st));
+      HIPC(c, c->variant == 1 ? launch_pass(a, blocks, st) : launch_pass_w8(a, blocks, st));
       if (prof) {
         HIPC(c, hipEventRecord(c->prof_ev[prof_used + 1], st));
         prof_used += 2;
       }
       ++launches;
     }
-    HIPC(c, hipMemcpyAsync(c->h_count, counts[p % 3], sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPC(c, hipMemcpyAsync(c->h_count, counts[p % 3], sizeof(uint32_t) * kShards,
+                           hipMemcpyDeviceToHost, st));
     HIPC(c, hipStreamSynchronize(st));
-    if (*c->h_count == 0) break;
+    uint64_t pending = 0;
+    for (int q = 0; q < kShards; ++q) pending += c->h_count[q];
+    if (pending == 0) break;
     if (p >= max_passes) {
       c->last_error = "pass cap reached before convergence";
       c->epoch_base = eb + (uint32_t)p + 4u;
@@ -192,8 +201,13 @@ int solve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t 
     }
   }
   if (stats) {
-    unsigned long long h[kStatSlots];
-    HIPC(c, hipMemcpy(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost));
+    unsigned long long hs[kShards * kStatSlots];
+    HIPC(c, hipMemcpy(hs, c->d_stats, sizeof hs, hipMemcpyDeviceToHost));
+    unsigned long long h[kStatSlots] = {0};
+    for (int q = 0; q < kShards; ++q)
+      for (int k = 0; k < kStatSlots; ++k)
+        h[k] = (k == kStatMaxActive) ? std::max(h[k], hs[q * kStatSlots + k])
+                                     : h[k] + hs[q * kStatSlots + k];
     std::memset(stats, 0, sizeof *stats);
     stats->passes = h[kStatPasses];
     stats->launches = launches;
@@ -202,8 +216,8 @@ int solve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t 
     stats->max_active = h[kStatMaxActive];
     stats->rounds = 0;
     stats->ms = ms;
-    stats->tile_w = kTileW;
-    stats->tile_h = kTileH;
+    stats->tile_w = TWd;
+    stats->tile_h = THd;
   }
   return DYMU_OK;
 }
@@ -264,9 +278,11 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
   }
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-  if (e == hipSuccess) e = hipMalloc(&c->d_counts, 64);
-  if (e == hipSuccess) e = hipMalloc(&c->d_stats, sizeof(unsigned long long) * kStatSlots);
-  if (e == hipSuccess) e = hipHostMalloc(&c->h_count, 64, hipHostMallocDefault);
+  if (const char* kv = std::getenv("DYMU_KERNEL")) c->variant = std::atoi(kv) == 1 ? 1 : 2;
+  if (e == hipSuccess) e = hipMalloc(&c->d_counts, sizeof(uint32_t) * 4 * kShards);
+  if (e == hipSuccess)
+    e = hipMalloc(&c->d_stats, sizeof(unsigned long long) * kShards * kStatSlots);
+  if (e == hipSuccess) e = hipHostMalloc(&c->h_count, sizeof(uint32_t) * 4 * kShards, hipHostMallocDefault);
   if (e != hipSuccess) {
     dymu_destroy(c);
     return e == hipErrorOutOfMemory ? DYMU_ERR_NOMEM : DYMU_ERR_HIP;

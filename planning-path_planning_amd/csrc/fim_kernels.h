@@ -6,8 +6,10 @@
 
 namespace dymu {
 
-constexpr int kTileW = 32;  // tile width  (x, columns)
-constexpr int kTileH = 32;  // tile height (y, rows)
+constexpr int kTileW = 32;  // v1 tile width  (x, columns)
+constexpr int kTileH = 32;  // v1 tile height (y, rows)
+constexpr int kWaveTile = 8;  // v2: one 64-lane wave owns an 8x8 tile, one cell per lane
+constexpr int kShards = 16;   // active lists are split in shards to spread the append atomics
 
 enum StatSlot : int {
   kStatPasses = 0,
@@ -27,13 +29,14 @@ struct PassArgs {
   int ghost_hi;     // row ny exists in memory (requires ny % kTileH == 0)
   int max_inner;    // cap on in-tile sweeps per visit
   uint32_t epoch;   // epoch stamped on tiles enqueued for the NEXT pass
-  const uint32_t* list_in;
-  const uint32_t* count_in;
+  uint32_t shard_cap;  // capacity of one shard (= number of tiles)
+  const uint32_t* list_in;   // kShards shards of shard_cap entries
+  const uint32_t* count_in;  // kShards counters
   uint32_t* list_out;
   uint32_t* count_out;
   uint32_t* count_clear;
   uint32_t* tile_epoch;
-  unsigned long long* stats;
+  unsigned long long* stats;  // kShards x kStatSlots
 };
 
 hipError_t launch_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, int64_t row_hi,
@@ -41,7 +44,8 @@ hipError_t launch_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, 
 hipError_t launch_seed(double* T, uint64_t ld, int64_t gi, int64_t gj, uint32_t* list,
                        uint32_t* count, uint32_t* tile_epoch, uint32_t epoch, uint32_t tile,
                        int set_goal, hipStream_t st);
-hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st);
+hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st);        // v1: 32x32 tile / workgroup
+hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st);     // v2: 8x8 tile / wave
 hipError_t launch_synth(double* F, uint64_t ld, uint32_t nx, uint32_t ny, uint64_t row0,
                         uint64_t seed, double frac, uint64_t oseed, int64_t gi, int64_t gj,
                         hipStream_t st);

@@ -21,6 +21,10 @@ namespace dymu {
 
 __device__ __forceinline__ double dinf() { return __builtin_inf(); }
 
+// fmin for operands that are never NaN (T values are >= 0 or +inf): a plain
+// compare-select, so the compiler does not canonicalise both inputs first.
+__device__ __forceinline__ double minnn(double a, double b) { return b < a ? b : a; }
+
 // Reference :504-535.  Tx = fmin(W,E), Ty = fmin(N,S); off-grid neighbours
 // are +inf (a NULL nb4 makes the reference use the other one alone, :508-523).
 // 2*pow(C,2.0) - pow(Tx-Ty,2.0) with pow(x,2.0) == x*x; no contraction.
@@ -31,7 +35,7 @@ __device__ __forceinline__ double eikonal(double tx, double ty, double c) {
     const double r = 2.0 * cc - d * d;
     return (tx + ty + sqrt(r)) / 2;
   }
-  return fmin(tx, ty) + c;
+  return minnn(tx, ty) + c;
 }
 
 // ---------------------------------------------------------------------------
@@ -105,6 +109,7 @@ __global__ __launch_bounds__(256) void k_fim_pass(PassArgs a) {
 
   if (blockIdx.x == 0 && tid == 0) {
     *a.count_clear = 0u;  // list (p+2)%3: read by pass p-1 (finished), appended by pass p+1
+    for (int q = 1; q < kShards; ++q) a.count_clear[q] = 0u;
     if (n_active > 0) {
       atomicAdd(&a.stats[kStatPasses], 1ull);
       atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
@@ -223,6 +228,176 @@ __global__ __launch_bounds__(256) void k_fim_pass(PassArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// v2 pass kernel: one 64-lane wave owns one 8x8 tile, one cell per lane
+// (lane = 8*r + c).  Each sweep writes the wave's cells into a per-wave 10x10
+// LDS image that also holds the tile's halo ring, and reads the four
+// neighbours back (in-wave LDS ops execute in order, so no barrier).  The wave relaxes Jacobi sweeps until
+// no lane improves (wave ballot: no barriers at all), so a workgroup's four
+// waves are four independent workers.  Enqueues are aggregated per workgroup
+// in LDS and published with one atomic per workgroup per pass into one of
+// kShards list shards (same-address atomics serialise at ~11 ns each).
+// ---------------------------------------------------------------------------
+constexpr int WT = kWaveTile;
+constexpr int QCAP = 1024;  // LDS enqueue buffer per workgroup
+
+// shard of a logical list index: the counters are prefix-summed in LDS.
+__device__ __forceinline__ uint32_t list_at(const uint32_t* list, uint32_t cap,
+                                            const uint32_t* pref, uint32_t li) {
+  int k = 0;
+#pragma unroll
+  for (int q = 1; q < kShards; ++q) k += (li >= pref[q]) ? 1 : 0;
+  return list[(uint64_t)k * cap + (li - pref[k])];
+}
+
+__global__ __launch_bounds__(256) void k_fim_pass_w8(PassArgs a) {
+  __shared__ uint32_t s_q[QCAP];
+  __shared__ uint32_t s_pref[kShards + 1];
+  __shared__ uint32_t s_nq, s_base;
+  __shared__ unsigned long long s_visits, s_sweeps;
+  // per-wave 10x10 image of the tile with its halo ring (corners unused)
+  __shared__ double s_img[4][(WT + 2) * (WT + 2)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int r = lane >> 3, c = lane & 7;
+  const uint32_t shard = blockIdx.x % kShards;
+
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int q = 0; q < kShards; ++q) {
+      s_pref[q] = acc;
+      acc += a.count_in[q];
+    }
+    s_pref[kShards] = acc;
+    s_nq = 0;
+    s_visits = 0;
+    s_sweeps = 0;
+  }
+  __syncthreads();
+  const uint32_t n_active = s_pref[kShards];
+  if (blockIdx.x == 0) {
+    if (tid < kShards) a.count_clear[tid] = 0u;
+    if (tid == 0 && n_active > 0) {
+      atomicAdd(&a.stats[kStatPasses], 1ull);
+      atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
+    }
+  }
+
+  unsigned long long my_visits = 0, my_sweeps = 0;
+  double* img = s_img[wv];
+  const int me = (r + 1) * (WT + 2) + (c + 1);  // own slot in the image
+  const uint32_t nwaves = gridDim.x * 4u;
+  for (uint32_t li = blockIdx.x * 4u + (uint32_t)wv; li < n_active; li += nwaves) {
+    const uint32_t tile = list_at(a.list_in, a.shard_cap, s_pref, li);
+    const int tx = (int)(tile % (uint32_t)a.ntx);
+    const int ty = (int)(tile / (uint32_t)a.ntx);
+    const int64_t i0 = (int64_t)tx * WT, j0 = (int64_t)ty * WT;
+    const int64_t gi = i0 + c, gj = j0 + r;
+    const bool inside = gi < a.nx && gj < a.ny;
+    double t = dinf(), f = dinf();
+    if (inside) {
+      const int64_t off = gj * a.ld + gi;
+      t = a.T[off];
+      f = a.F[off];
+    }
+    // halo ring: lane (r,c) with c==0 / c==7 loads the west / east cell of its
+    // row, lane with r==0 / r==7 the south / north cell of its column.
+    double hx = dinf(), hy = dinf();
+    if (gj < a.ny) {
+      if (c == 0 && i0 > 0) hx = a.T[gj * a.ld + (i0 - 1)];
+      if (c == WT - 1 && i0 + WT < a.nx) hx = a.T[gj * a.ld + (i0 + WT)];
+    }
+    if (gi < a.nx) {
+      if (r == 0 && (j0 > 0 || a.ghost_lo)) hy = a.T[(j0 - 1) * a.ld + gi];
+      if (r == WT - 1) {
+        const int64_t jn = j0 + WT;
+        if (jn < a.ny || (jn == a.ny && a.ghost_hi)) hy = a.T[jn * a.ld + gi];
+      }
+    }
+    if (c == 0) img[me - 1] = hx;
+    if (c == WT - 1) img[me + 1] = hx;
+    if (r == 0) img[me - (WT + 2)] = hy;
+    if (r == WT - 1) img[me + (WT + 2)] = hy;
+    const double t0 = t;
+    int sweeps = 0;
+    bool capped = true;
+    while (sweeps < a.max_inner) {
+      img[me] = t;
+      __builtin_amdgcn_wave_barrier();
+      const double south = img[me - (WT + 2)];
+      const double west = img[me - 1];
+      const double east = img[me + 1];
+      const double north = img[me + (WT + 2)];
+      const double tx_ = minnn(west, east), ty_ = minnn(north, south);
+      bool imp = false;
+      // cheap bound: U >= min(Tx,Ty) + C/sqrt(2) (exact arithmetic); 0.7071 < 1/sqrt(2)
+      // leaves a relative margin ~1e-5*C, far above rounding, so a skipped cell can
+      // never have improved.
+      if (minnn(tx_, ty_) + 0.7071 * f < t) {
+        const double u = eikonal(tx_, ty_, f);  // :531-535
+        if (u < t) {                            // :537
+          t = u;
+          imp = true;
+        }
+      }
+      ++sweeps;
+      __builtin_amdgcn_wave_barrier();
+      if (!__any(imp)) {
+        capped = false;
+        break;
+      }
+    }
+    my_visits += 1;
+    my_sweeps += (unsigned long long)sweeps;
+
+    const bool dec = t < t0;
+    if (dec) a.T[gj * a.ld + gi] = t;
+    const unsigned long long m = __ballot(dec);
+    // lanes 0..4 test one neighbour each: S, W, E, N, self
+    bool want = false;
+    int nx_t = tx, ny_t = ty;
+    if (lane == 0) { want = (m & 0xFFull) && ty > 0; ny_t = ty - 1; }
+    else if (lane == 1) { want = (m & 0x0101010101010101ull) && tx > 0; nx_t = tx - 1; }
+    else if (lane == 2) { want = (m & 0x8080808080808080ull) && tx + 1 < a.ntx; nx_t = tx + 1; }
+    else if (lane == 3) { want = (m & 0xFF00000000000000ull) && ty + 1 < a.nty; ny_t = ty + 1; }
+    else if (lane == 4) { want = capped; }
+    if (want) {
+      const uint32_t nt = (uint32_t)ny_t * (uint32_t)a.ntx + (uint32_t)nx_t;
+      // a plain read filters most duplicates before the atomic decides
+      if (a.tile_epoch[nt] < a.epoch && atomicMax(&a.tile_epoch[nt], a.epoch) < a.epoch) {
+        const uint32_t pos = atomicAdd(&s_nq, 1u);
+        if (pos < QCAP) {
+          s_q[pos] = nt;
+        } else {  // overflow: publish directly
+          const uint32_t gp = atomicAdd(&a.count_out[shard], 1u);
+          a.list_out[(uint64_t)shard * a.shard_cap + gp] = nt;
+        }
+      }
+    }
+  }
+  // per-workgroup publication
+  if (lane == 0 && my_visits) {
+    atomicAdd(&s_visits, my_visits);
+    atomicAdd(&s_sweeps, my_sweeps);
+  }
+  __syncthreads();
+  const uint32_t nq = s_nq < QCAP ? s_nq : QCAP;
+  if (tid == 0) {
+    if (nq) s_base = atomicAdd(&a.count_out[shard], nq);
+    if (s_visits) {
+      unsigned long long* st = a.stats + (uint64_t)shard * kStatSlots;
+      atomicAdd(&st[kStatVisits], s_visits);
+      atomicAdd(&st[kStatSweeps], s_sweeps);
+    }
+  }
+  __syncthreads();
+  for (uint32_t q = tid; q < nq; q += blockDim.x)
+    a.list_out[(uint64_t)shard * a.shard_cap + s_base + q] = s_q[q];
+}
+
 // ---------------------------------------------------------------------------
 // Synthetic speed field; k = global row-major index.
 // ---------------------------------------------------------------------------
@@ -277,6 +452,11 @@ hipError_t launch_seed(double* T, uint64_t ld, int64_t gi, int64_t gj, uint32_t*
 
 hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st) {
   hipLaunchKernelGGL(k_fim_pass, dim3(blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_fim_pass_w8, dim3(blocks), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
