@@ -28,8 +28,6 @@ sys.path.insert(0, os.path.join(ROOT, "planning-path_planning_amd"))
 
 import numpy as np  # noqa: E402
 
-import dymu  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
 BYTES_PER_CELL_VISIT = 24  # read T 8 + read F 8 + write T 8
 BYTES_PER_CELL_SOLVE = 16  # read F once + write T once
@@ -46,6 +44,9 @@ def parse():
                     help="edge of the grid the CPU baseline solves (0 = skip)")
     ap.add_argument("--no-profile", action="store_true",
                     help="no per-launch events (roofline reported as null)")
+    ap.add_argument("--backend", default="nccl",
+                    help="N>1 only: 'nccl' (RCCL over xGMI) or 'gloo' (host-staged rehearsal)")
+    ap.add_argument("--passes-per-exchange", type=int, default=4)
     return ap.parse_args()
 
 
@@ -72,6 +73,8 @@ def cpu_baseline(n_edge, obst):
 
 
 def run_single(args):
+    import dymu
+
     N = args.size
     eng = dymu.Engine(device=int(os.environ.get("LOCAL_RANK", "0")))
     n = N * N
@@ -108,6 +111,7 @@ def main():
     world = args.gpus
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
+        import torch  # noqa: F401  (before dymu: one HIP runtime in the process)
         import bench_sharded
 
         res = bench_sharded.run(args)
@@ -156,7 +160,8 @@ def main():
             "workload": f"config 3: {N}x{N} grid, {world}x MI355X, splitmix64 U(1,5) speed, "
                         f"{args.obst:.0%} iid obstacles, goal centre, full solve",
             "grid": N,
-            "parallelism": "single" if world == 1 else f"row-slab x{world}",
+            "parallelism": "single" if world == 1 else f"row-slab x{world} ({args.backend})",
+            "exchange_rounds_per_solve": tot.get("rounds", 0) / K,
             "passes_per_solve": tot["passes"] / K,
             "tile_visits_per_solve": tot["tile_visits"] / K,
             "inner_sweeps_per_solve": tot["inner_sweeps"] / K,

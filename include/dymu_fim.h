@@ -85,6 +85,43 @@ int dymu_solve_device(dymu_ctx* ctx, const double* dF, double* dT, uint32_t nx, 
                       uint64_t ld, uint32_t goal_i, uint32_t goal_j, void* stream,
                       dymu_stats* stats);
 
+/* ---- row-slab domains (multi-GPU sharding; also single-GPU virtual slabs) ----
+ * A rank owns rows [row0, row0+nrows) of an nx-wide global grid.  T points at
+ * its first owned row; with ghost_lo the row above it (T - ld) holds the
+ * neighbour rank's last row, with ghost_hi the row T + nrows*ld holds the
+ * next rank's first row (then nrows must be a multiple of 32).  Ghost rows are
+ * read-only halo for the kernels.  Protocol (bench_sharded.py / dymu.sharded):
+ *   dymu_dom_begin -> repeat { dymu_dom_run(K passes); exchange boundary rows
+ *   (RCCL); dymu_dom_merge_ghosts(received rows) } until the all-reduced
+ *   pending count is 0 -> dymu_dom_finish.
+ * All calls except dymu_dom_pending / dymu_dom_finish are asynchronous on
+ * `stream`. */
+typedef struct dymu_domain {
+  const double* F; /* owned rows, pitch ld (device) */
+  double* T;       /* owned row 0 (device); ghost rows at T - ld / T + nrows*ld */
+  uint64_t ld;
+  uint32_t nx, nrows;
+  int32_t ghost_lo, ghost_hi;
+} dymu_domain;
+
+/* Partition ny rows over nranks slabs (boundaries on multiples of 32 rows). */
+int dymu_slab_rows(uint32_t ny, uint32_t nranks, uint32_t rank, uint32_t* row0, uint32_t* nrows);
+/* Initialise T (owned + ghost rows = +inf) and seed the goal if it lies in
+ * this slab (goal_j_local = goal row - row0, or -1). */
+int dymu_dom_begin(dymu_ctx* ctx, const dymu_domain* dom, int64_t goal_i, int64_t goal_j_local,
+                   void* stream);
+/* Launch `passes` FIM passes (speculative passes with no active tile are cheap). */
+int dymu_dom_run(dymu_ctx* ctx, uint32_t passes, void* stream);
+/* Min-merge received neighbour rows (device pointers, nx doubles, or NULL)
+ * into the ghost rows and queue the tiles under improved columns; if
+ * d_pending != NULL also write the number of queued tiles there (int32). */
+int dymu_dom_merge_ghosts(dymu_ctx* ctx, const double* new_lo, const double* new_hi,
+                          int32_t* d_pending, void* stream);
+/* Tiles queued for the next pass (synchronises `stream`). */
+int dymu_dom_pending(dymu_ctx* ctx, void* stream, uint64_t* pending);
+/* End the domain solve; fills stats (passes, visits, sweeps). */
+int dymu_dom_finish(dymu_ctx* ctx, void* stream, dymu_stats* stats);
+
 /* Synthetic input generator on the device (bench/test data):
  *   F[k] = 1 + 4*u(seed, k),  u(s,k) = (splitmix64(s ^ k) >> 11) * 2^-53,
  *   obstacle (F = +inf) where u(obst_seed, k) < obst_frac, except the 3x3

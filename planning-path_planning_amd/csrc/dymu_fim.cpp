@@ -45,6 +45,21 @@ struct dymu_ctx {
   double* d_T = nullptr;
   uint64_t cells_cap = 0;
 
+  // current domain (whole grid or one row slab) being solved
+  struct Dom {
+    bool live = false;
+    PassArgs a{};
+    uint32_t ntiles = 0;
+    uint32_t eb = 0;
+    uint64_t p = 0;         // next pass index
+    uint64_t launches = 0;
+    uint64_t max_passes = 0;
+    int blocks = 0;
+    uint32_t* lists[3] = {nullptr, nullptr, nullptr};
+    uint32_t* counts[3] = {nullptr, nullptr, nullptr};
+    size_t prof_used = 0;
+  } dom;
+
   // profiling
   int profiling = 0;
   std::vector<hipEvent_t> prof_ev;
@@ -101,100 +116,126 @@ int ensure_cells(dymu_ctx* c, uint64_t cells) {
 int tile_w(const dymu_ctx* c) { return c->variant == 1 ? kTileW : kWaveTile; }
 int tile_h(const dymu_ctx* c) { return c->variant == 1 ? kTileH : kWaveTile; }
 
-int solve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
-               uint32_t gi, uint32_t gj, hipStream_t st, dymu_stats* stats) {
-  if (!dF || !dT || nx == 0 || ny == 0 || ld < nx || gi >= nx || gj >= ny) return DYMU_ERR_ARG;
+// ---- domain primitives (whole grid, or one row slab with ghost rows) ----
+int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t nrows, uint64_t ld,
+              int ghost_lo, int ghost_hi, int64_t gi, int64_t gj, hipStream_t st) {
+  if (!dF || !dT || nx == 0 || nrows == 0 || ld < nx) return DYMU_ERR_ARG;
   const int TWd = tile_w(c), THd = tile_h(c);
-  const uint32_t ntx = (uint32_t)((nx + TWd - 1) / TWd), nty = (uint32_t)((ny + THd - 1) / THd);
+  if (ghost_hi && (nrows % (uint32_t)THd) != 0) return DYMU_ERR_ARG;
+  if (gj >= 0 && (gi < 0 || gi >= (int64_t)nx || gj >= (int64_t)nrows)) return DYMU_ERR_ARG;
+  const uint32_t ntx = (uint32_t)((nx + TWd - 1) / TWd), nty = (uint32_t)((nrows + THd - 1) / THd);
   const uint64_t ntiles64 = (uint64_t)ntx * nty;
   if (ntiles64 >= (1ull << 31)) return DYMU_ERR_ARG;
   const uint32_t ntiles = (uint32_t)ntiles64;
   int rc = ensure_tiles(c, ntiles);
   if (rc) return rc;
-
-  const uint64_t max_passes =
-      c->opts.max_passes > 0 ? (uint64_t)c->opts.max_passes : 4ull * ntiles + 1024ull;
-  if ((uint64_t)c->epoch_base + max_passes + 8 >= 0xFFFFFFF0ull) {
+  auto& D = c->dom;
+  D = dymu_ctx::Dom{};
+  D.ntiles = ntiles;
+  D.max_passes = c->opts.max_passes > 0 ? (uint64_t)c->opts.max_passes : 4ull * ntiles + 1024ull;
+  if ((uint64_t)c->epoch_base + D.max_passes + 8 >= 0xFFFFFFF0ull) {
     HIPC(c, hipMemsetAsync(c->d_tile_epoch, 0, sizeof(uint32_t) * (uint64_t)ntiles, st));
     c->epoch_base = 0;
   }
-  const uint32_t eb = c->epoch_base;
+  D.eb = c->epoch_base;
   const uint64_t lstride = (uint64_t)kShards * ntiles;
-  uint32_t* lists[3] = {c->d_lists, c->d_lists + lstride, c->d_lists + 2 * lstride};
-  uint32_t* counts[3] = {c->d_counts, c->d_counts + kShards, c->d_counts + 2 * kShards};
+  for (int q = 0; q < 3; ++q) {
+    D.lists[q] = c->d_lists + q * lstride;
+    D.counts[q] = c->d_counts + q * kShards;
+  }
   HIPC(c, hipMemsetAsync(c->d_counts, 0, sizeof(uint32_t) * 3 * kShards, st));
   HIPC(c, hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * kShards * kStatSlots, st));
-  HIPC(c, launch_fill_inf(dT, ld, nx, 0, ny, st));
-  const uint32_t gtile = (gj / THd) * ntx + (gi / TWd);
-  HIPC(c, launch_seed(dT, ld, gi, gj, lists[0], counts[0], c->d_tile_epoch, eb + 1, gtile, 1, st));
-
-  PassArgs a{};
+  HIPC(c, launch_fill_inf(dT, ld, nx, ghost_lo ? -1 : 0, (int64_t)nrows + (ghost_hi ? 1 : 0), st));
+  if (gj >= 0) {
+    const uint32_t gtile = (uint32_t)(gj / THd) * ntx + (uint32_t)(gi / TWd);
+    HIPC(c, launch_seed(dT, ld, gi, gj, D.lists[0], D.counts[0], c->d_tile_epoch, D.eb + 1, gtile,
+                        1, st));
+  }
+  PassArgs& a = D.a;
   a.F = dF;
   a.T = dT;
   a.ld = (int64_t)ld;
   a.nx = nx;
-  a.ny = ny;
+  a.ny = nrows;
   a.ntx = (int)ntx;
   a.nty = (int)nty;
-  a.ghost_lo = 0;
-  a.ghost_hi = 0;
+  a.ghost_lo = ghost_lo;
+  a.ghost_hi = ghost_hi;
   a.max_inner = c->opts.max_inner > 0 ? c->opts.max_inner : 4 * (TWd + THd);
   a.shard_cap = ntiles;
   a.tile_epoch = c->d_tile_epoch;
   a.stats = c->d_stats;
-  const int blocks = c->opts.grid_blocks > 0 ? c->opts.grid_blocks : c->cu_count * 8;
+  D.blocks = c->opts.grid_blocks > 0 ? c->opts.grid_blocks : c->cu_count * 8;
+  D.live = true;
+  return DYMU_OK;
+}
 
+int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
+  auto& D = c->dom;
+  if (!D.live) return DYMU_ERR_STATE;
+  PassArgs& a = D.a;
   const bool prof = c->profiling != 0;
-  size_t prof_used = 0;
-  HIPC(c, hipEventRecord(c->ev0, st));
-  uint64_t p = 0, launches = 0;
-  uint64_t K = c->opts.passes_per_check > 0 ? (uint64_t)c->opts.passes_per_check : 4;
-  for (;;) {
-    for (uint64_t k = 0; k < K; ++k, ++p) {
-      a.list_in = lists[p % 3];
-      a.count_in = counts[p % 3];
-      a.list_out = lists[(p + 1) % 3];
-      a.count_out = counts[(p + 1) % 3];
-      a.count_clear = counts[(p + 2) % 3];
-      a.epoch = eb + (uint32_t)p + 2u;
-      if (prof) {
-        while (c->prof_ev.size() < prof_used + 2) {
-          hipEvent_t e;
-          HIPC(c, hipEventCreate(&e));
-          c->prof_ev.push_back(e);
-        }
-        HIPC(c, hipEventRecord(c->prof_ev[prof_used], st));
+  for (uint64_t k = 0; k < K; ++k, ++D.p) {
+    const uint64_t p = D.p;
+    a.list_in = D.lists[p % 3];
+    a.count_in = D.counts[p % 3];
+    a.list_out = D.lists[(p + 1) % 3];
+    a.count_out = D.counts[(p + 1) % 3];
+    a.count_clear = D.counts[(p + 2) % 3];
+    a.epoch = D.eb + (uint32_t)p + 2u;
+    if (prof) {
+      while (c->prof_ev.size() < D.prof_used + 2) {
+        hipEvent_t e;
+        HIPC(c, hipEventCreate(&e));
+        c->prof_ev.push_back(e);
       }
-      HIPC(c, c->variant == 1 ? launch_pass(a, blocks, st) : launch_pass_w8(a, blocks, st));
-      if (prof) {
-        HIPC(c, hipEventRecord(c->prof_ev[prof_used + 1], st));
-        prof_used += 2;
-      }
-      ++launches;
+      HIPC(c, hipEventRecord(c->prof_ev[D.prof_used], st));
     }
-    HIPC(c, hipMemcpyAsync(c->h_count, counts[p % 3], sizeof(uint32_t) * kShards,
-                           hipMemcpyDeviceToHost, st));
-    HIPC(c, hipStreamSynchronize(st));
-    uint64_t pending = 0;
-    for (int q = 0; q < kShards; ++q) pending += c->h_count[q];
-    if (pending == 0) break;
-    if (p >= max_passes) {
-      c->last_error = "pass cap reached before convergence";
-      c->epoch_base = eb + (uint32_t)p + 4u;
-      return DYMU_ERR_NOT_CONVERGED;
+    HIPC(c, c->variant == 1 ? launch_pass(a, D.blocks, st) : launch_pass_w8(a, D.blocks, st));
+    if (prof) {
+      HIPC(c, hipEventRecord(c->prof_ev[D.prof_used + 1], st));
+      D.prof_used += 2;
     }
-    if (c->opts.passes_per_check <= 0) K = std::min<uint64_t>(K * 2, 64);
+    ++D.launches;
   }
-  HIPC(c, hipEventRecord(c->ev1, st));
-  HIPC(c, hipEventSynchronize(c->ev1));
-  c->epoch_base = eb + (uint32_t)p + 4u;
+  return DYMU_OK;
+}
 
-  float ms = 0.f;
-  HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
-  c->last_launches = launches;
+// tiles queued for the next pass (synchronises the stream)
+int dom_pending(dymu_ctx* c, hipStream_t st, uint64_t* out) {
+  auto& D = c->dom;
+  if (!D.live) return DYMU_ERR_STATE;
+  HIPC(c, hipMemcpyAsync(c->h_count, D.counts[D.p % 3], sizeof(uint32_t) * kShards,
+                         hipMemcpyDeviceToHost, st));
+  HIPC(c, hipStreamSynchronize(st));
+  uint64_t pending = 0;
+  for (int q = 0; q < kShards; ++q) pending += c->h_count[q];
+  *out = pending;
+  return DYMU_OK;
+}
+
+int dom_merge(dymu_ctx* c, const double* lo, const double* hi, int32_t* d_pending, hipStream_t st) {
+  auto& D = c->dom;
+  if (!D.live) return DYMU_ERR_STATE;
+  if ((lo && !D.a.ghost_lo) || (hi && !D.a.ghost_hi)) return DYMU_ERR_ARG;
+  const uint64_t p = D.p;
+  if (lo || hi)
+    HIPC(c, launch_merge_ghosts(D.a.T, D.a.ld, D.a.nx, D.a.ny, lo, hi, D.a.ntx, D.a.nty,
+                                tile_w(c), D.lists[p % 3], D.counts[p % 3], D.ntiles,
+                                c->d_tile_epoch, D.eb + (uint32_t)p + 1u, st));
+  if (d_pending) HIPC(c, launch_sum_counts(D.counts[p % 3], d_pending, st));
+  return DYMU_OK;
+}
+
+int dom_finish(dymu_ctx* c, hipStream_t st, dymu_stats* stats, double ms) {
+  auto& D = c->dom;
+  if (!D.live) return DYMU_ERR_STATE;
+  HIPC(c, hipStreamSynchronize(st));
+  c->epoch_base = D.eb + (uint32_t)D.p + 4u;
+  c->last_launches = D.launches;
   c->last_pass_ms = 0.0;
-  if (prof) {
-    for (size_t q = 0; q + 1 < prof_used; q += 2) {
+  if (c->profiling) {
+    for (size_t q = 0; q + 1 < D.prof_used; q += 2) {
       float m = 0.f;
       HIPC(c, hipEventElapsedTime(&m, c->prof_ev[q], c->prof_ev[q + 1]));
       c->last_pass_ms += m;
@@ -210,16 +251,46 @@ int solve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t 
                                      : h[k] + hs[q * kStatSlots + k];
     std::memset(stats, 0, sizeof *stats);
     stats->passes = h[kStatPasses];
-    stats->launches = launches;
+    stats->launches = D.launches;
     stats->tile_visits = h[kStatVisits];
     stats->inner_sweeps = h[kStatSweeps];
     stats->max_active = h[kStatMaxActive];
     stats->rounds = 0;
     stats->ms = ms;
-    stats->tile_w = TWd;
-    stats->tile_h = THd;
+    stats->tile_w = tile_w(c);
+    stats->tile_h = tile_h(c);
   }
+  D.live = false;
   return DYMU_OK;
+}
+
+int solve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
+               uint32_t gi, uint32_t gj, hipStream_t st, dymu_stats* stats) {
+  if (gi >= nx || gj >= ny) return DYMU_ERR_ARG;
+  int rc = dom_begin(c, dF, dT, nx, ny, ld, 0, 0, gi, gj, st);
+  if (rc) return rc;
+  HIPC(c, hipEventRecord(c->ev0, st));
+  uint64_t K = c->opts.passes_per_check > 0 ? (uint64_t)c->opts.passes_per_check : 4;
+  for (;;) {
+    rc = dom_launch(c, K, st);
+    if (rc) return rc;
+    uint64_t pending = 0;
+    rc = dom_pending(c, st, &pending);
+    if (rc) return rc;
+    if (pending == 0) break;
+    if (c->dom.p >= c->dom.max_passes) {
+      c->last_error = "pass cap reached before convergence";
+      c->epoch_base = c->dom.eb + (uint32_t)c->dom.p + 4u;
+      c->dom.live = false;
+      return DYMU_ERR_NOT_CONVERGED;
+    }
+    if (c->opts.passes_per_check <= 0) K = std::min<uint64_t>(K * 2, 64);
+  }
+  HIPC(c, hipEventRecord(c->ev1, st));
+  HIPC(c, hipEventSynchronize(c->ev1));
+  float ms = 0.f;
+  HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  return dom_finish(c, st, stats, ms);
 }
 
 hipStream_t pick_stream(dymu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
@@ -368,6 +439,54 @@ int dymu_memcpy_h2d(dymu_ctx* c, void* dst, const void* src, size_t bytes) {
   if (!c) return DYMU_ERR_ARG;
   HIPC(c, hipSetDevice(c->device));
   HIPC(c, hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return DYMU_OK;
+}
+
+int dymu_dom_begin(dymu_ctx* c, const dymu_domain* d, int64_t goal_i, int64_t goal_j_local,
+                   void* stream) {
+  if (!c || !d) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  return dom_begin(c, d->F, d->T, d->nx, d->nrows, d->ld, d->ghost_lo, d->ghost_hi, goal_i,
+                   goal_j_local, pick_stream(c, stream));
+}
+
+int dymu_dom_run(dymu_ctx* c, uint32_t passes, void* stream) {
+  if (!c) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  return dom_launch(c, passes, pick_stream(c, stream));
+}
+
+int dymu_dom_merge_ghosts(dymu_ctx* c, const double* new_lo, const double* new_hi,
+                          int32_t* d_pending, void* stream) {
+  if (!c) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  return dom_merge(c, new_lo, new_hi, d_pending, pick_stream(c, stream));
+}
+
+int dymu_dom_pending(dymu_ctx* c, void* stream, uint64_t* pending) {
+  if (!c || !pending) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  return dom_pending(c, pick_stream(c, stream), pending);
+}
+
+int dymu_dom_finish(dymu_ctx* c, void* stream, dymu_stats* stats) {
+  if (!c) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  return dom_finish(c, pick_stream(c, stream), stats, 0.0);
+}
+
+int dymu_slab_rows(uint32_t ny, uint32_t nranks, uint32_t rank, uint32_t* row0, uint32_t* nrows) {
+  if (!row0 || !nrows || nranks == 0 || rank >= nranks) return DYMU_ERR_ARG;
+  // slab boundaries on multiples of 32 rows (a whole number of tile rows for
+  // every kernel variant), so every slab but the last satisfies ghost_hi.
+  const uint32_t A = 32;
+  const uint64_t blocks = ((uint64_t)ny + A - 1) / A;
+  const uint64_t b0 = blocks * rank / nranks, b1 = blocks * (rank + 1) / nranks;
+  uint64_t r0 = b0 * A, r1 = b1 * A;
+  if (r1 > ny) r1 = ny;
+  if (r0 > ny) r0 = ny;
+  *row0 = (uint32_t)r0;
+  *nrows = (uint32_t)(r1 - r0);
   return DYMU_OK;
 }
 

@@ -398,6 +398,54 @@ __global__ __launch_bounds__(256) void k_fim_pass_w8(PassArgs a) {
     a.list_out[(uint64_t)shard * a.shard_cap + s_base + q] = s_q[q];
 }
 
+
+// ---------------------------------------------------------------------------
+// Sharded (row-slab) mode: merge freshly received neighbour rows into the
+// ghost rows (values only decrease, so a min-merge) and seed the tiles of the
+// first / last tile row under every column that improved, into the list the
+// next pass reads.  Also used by the single-GPU virtual-slab tests.
+// ---------------------------------------------------------------------------
+__global__ void k_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,
+                               const double* new_lo, const double* new_hi, int ntx, int nty,
+                               int tile_w, uint32_t* list, uint32_t* counts, uint32_t cap,
+                               uint32_t* tile_epoch, uint32_t epoch) {
+  // blocks of 256 threads start at multiples of 256 columns and tile_w divides
+  // 64, so a tile's columns are tile_w consecutive lanes of one wave.
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const uint32_t shard = blockIdx.x % kShards;
+  const unsigned long long tmask = tile_w >= 64 ? ~0ull : ((1ull << tile_w) - 1ull);
+  for (int side = 0; side < 2; ++side) {
+    const double* src = side == 0 ? new_lo : new_hi;
+    if (!src) continue;  // uniform
+    bool seed = false;
+    if (k < nx) {
+      double* g = T + (side == 0 ? -ld : nrows * ld) + k;
+      const double v = src[k];
+      if (v < *g) {
+        *g = v;
+        seed = true;
+      }
+    }
+    const unsigned long long m = __ballot(seed);
+    if (k < nx && (k % tile_w) == 0 && ((m >> lane) & tmask)) {
+      const uint32_t tile = (uint32_t)((side == 0 ? 0 : nty - 1) * (int64_t)ntx + k / tile_w);
+      if (atomicMax(&tile_epoch[tile], epoch) < epoch) {
+        const uint32_t pos = atomicAdd(&counts[shard], 1u);
+        list[(uint64_t)shard * cap + pos] = tile;
+      }
+    }
+  }
+}
+
+__global__ void k_sum_counts(const uint32_t* counts, int32_t* out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    uint32_t s = 0;
+    for (int q = 0; q < kShards; ++q) s += counts[q];
+    *out = (int32_t)s;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Synthetic speed field; k = global row-major index.
 // ---------------------------------------------------------------------------
@@ -457,6 +505,22 @@ hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st) {
 
 hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st) {
   hipLaunchKernelGGL(k_fim_pass_w8, dim3(blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,
+                               const double* new_lo, const double* new_hi, int ntx, int nty,
+                               int tile_w, uint32_t* list, uint32_t* counts, uint32_t cap,
+                               uint32_t* tile_epoch, uint32_t epoch, hipStream_t st) {
+  const unsigned blocks = (unsigned)((nx + 255) / 256);
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_merge_ghosts, dim3(blocks), dim3(256), 0, st, T, ld, nx, nrows, new_lo,
+                     new_hi, ntx, nty, tile_w, list, counts, cap, tile_epoch, epoch);
+  return hipGetLastError();
+}
+
+hipError_t launch_sum_counts(const uint32_t* counts, int32_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_sum_counts, dim3(1), dim3(64), 0, st, counts, out);
   return hipGetLastError();
 }
 

@@ -49,6 +49,18 @@ class DymuOpts(ctypes.Structure):
     ]
 
 
+class DymuDomain(ctypes.Structure):
+    _fields_ = [
+        ("F", ctypes.c_void_p),
+        ("T", ctypes.c_void_p),
+        ("ld", ctypes.c_uint64),
+        ("nx", ctypes.c_uint32),
+        ("nrows", ctypes.c_uint32),
+        ("ghost_lo", ctypes.c_int32),
+        ("ghost_hi", ctypes.c_int32),
+    ]
+
+
 class DymuStats(ctypes.Structure):
     _fields_ = [
         ("passes", ctypes.c_uint64),
@@ -83,6 +95,12 @@ FIM_SYMBOLS = {
     "dymu_memcpy_d2h": (_i32, [_vp, _vp, _vp, ctypes.c_size_t]),
     "dymu_memcpy_h2d": (_i32, [_vp, _vp, _vp, ctypes.c_size_t]),
     "dymu_set_profiling": (_i32, [_vp, _i32]),
+    "dymu_slab_rows": (_i32, [_u32, _u32, _u32, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
+    "dymu_dom_begin": (_i32, [_vp, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, _vp]),
+    "dymu_dom_run": (_i32, [_vp, _u32, _vp]),
+    "dymu_dom_merge_ghosts": (_i32, [_vp, _vp, _vp, _vp, _vp]),
+    "dymu_dom_pending": (_i32, [_vp, _vp, ctypes.POINTER(_u64)]),
+    "dymu_dom_finish": (_i32, [_vp, _vp, ctypes.POINTER(DymuStats)]),
     "dymu_last_pass_timing": (_i32, [_vp, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_uint64)]),
     "dymu_strerror": (ctypes.c_char_p, [_i32]),
@@ -201,6 +219,32 @@ class Engine:
         src = np.ascontiguousarray(src)
         _check(self._lib.dymu_memcpy_h2d(self.ctx, dst, src.ctypes.data, src.nbytes), self.ctx)
 
+    # -- row-slab domain primitives (multi-GPU sharding, dymu.sharded) --
+    def dom_begin(self, F: int, T: int, nx: int, nrows: int, ld: int, ghost_lo: bool,
+                  ghost_hi: bool, goal_i: int, goal_j_local: int, stream: int = 0):
+        d = DymuDomain(F, T, ld, nx, nrows, int(ghost_lo), int(ghost_hi))
+        self._dom = d  # keep alive
+        _check(self._lib.dymu_dom_begin(self.ctx, ctypes.addressof(d), goal_i, goal_j_local,
+                                        stream or None), self.ctx)
+
+    def dom_run(self, passes: int, stream: int = 0):
+        _check(self._lib.dymu_dom_run(self.ctx, passes, stream or None), self.ctx)
+
+    def dom_merge_ghosts(self, new_lo: int = 0, new_hi: int = 0, pending: int = 0,
+                         stream: int = 0):
+        _check(self._lib.dymu_dom_merge_ghosts(self.ctx, new_lo or None, new_hi or None,
+                                               pending or None, stream or None), self.ctx)
+
+    def dom_pending(self, stream: int = 0) -> int:
+        n = ctypes.c_uint64()
+        _check(self._lib.dymu_dom_pending(self.ctx, stream or None, ctypes.byref(n)), self.ctx)
+        return n.value
+
+    def dom_finish(self, stream: int = 0) -> dict:
+        st = DymuStats()
+        _check(self._lib.dymu_dom_finish(self.ctx, stream or None, ctypes.byref(st)), self.ctx)
+        return st.as_dict()
+
     def set_profiling(self, on: bool):
         _check(self._lib.dymu_set_profiling(self.ctx, 1 if on else 0), self.ctx)
 
@@ -209,6 +253,13 @@ class Engine:
         _check(self._lib.dymu_last_pass_timing(self.ctx, ctypes.byref(ms), ctypes.byref(n)),
                self.ctx)
         return ms.value, n.value
+
+
+def slab_rows(ny: int, nranks: int, rank: int):
+    """(row0, nrows) of `rank`'s row slab (boundaries on multiples of 32 rows)."""
+    r0, n = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(load_fim().dymu_slab_rows(ny, nranks, rank, ctypes.byref(r0), ctypes.byref(n)))
+    return r0.value, n.value
 
 
 def device_count() -> int:

@@ -1,0 +1,70 @@
+"""Row-slab domains on ONE GPU ("virtual slabs"): S engines,
+each owning a slab with ghost rows, exchanging boundary rows through the host
+until no slab has queued tiles.  The stitched map must equal the oracle FMM,
+i.e. the sharded fixed point is the single-GPU one."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def solve_virtual_slabs(dymu, F, goal, S, K=8):
+    ny, nx = F.shape
+    slabs = []
+    for s in range(S):
+        row0, nrows = dymu.slab_rows(ny, S, s)
+        eng = dymu.Engine()
+        dF = eng.alloc(8 * nrows * nx)
+        dT = eng.alloc(8 * (nrows + 2) * nx)
+        stage = eng.alloc(16 * nx)
+        eng.h2d(dF, np.ascontiguousarray(F[row0:row0 + nrows]))
+        lo, hi = s > 0, s < S - 1
+        gl = goal[1] - row0 if row0 <= goal[1] < row0 + nrows else -1
+        eng.dom_begin(dF, dT + 8 * nx, nx, nrows, nx, lo, hi, goal[0] if gl >= 0 else 0, gl)
+        slabs.append(dict(eng=eng, row0=row0, nrows=nrows, dF=dF, dT=dT, stage=stage, lo=lo,
+                          hi=hi))
+    rounds = 0
+    row = np.empty(nx)
+    while True:
+        rounds += 1
+        for sl in slabs:
+            sl["eng"].dom_run(K)
+        # boundary rows out (first / last owned rows), into neighbours' staging
+        for s, sl in enumerate(slabs):
+            e = sl["eng"]
+            if sl["lo"]:
+                e.d2h(row, sl["dT"] + 8 * nx)              # my first owned row
+                slabs[s - 1]["eng"].h2d(slabs[s - 1]["stage"] + 8 * nx, row)   # their hi stage
+            if sl["hi"]:
+                e.d2h(row, sl["dT"] + 8 * nx * sl["nrows"])  # my last owned row
+                slabs[s + 1]["eng"].h2d(slabs[s + 1]["stage"], row)            # their lo stage
+        pending = 0
+        for sl in slabs:
+            sl["eng"].dom_merge_ghosts(sl["stage"] if sl["lo"] else 0,
+                                       sl["stage"] + 8 * nx if sl["hi"] else 0, 0)
+            pending += sl["eng"].dom_pending()
+        if pending == 0 or rounds > 100000:
+            break
+    T = np.empty((ny, nx))
+    for sl in slabs:
+        buf = np.empty((sl["nrows"], nx))
+        sl["eng"].d2h(buf, sl["dT"] + 8 * nx)
+        T[sl["row0"]:sl["row0"] + sl["nrows"]] = buf
+        sl["eng"].dom_finish()
+        for k in ("dF", "dT", "stage"):
+            sl["eng"].free(sl[k])
+        sl["eng"].close()
+    return T, rounds
+
+
+@pytest.mark.parametrize("S,nx,ny,goal,frac", [(2, 200, 160, (100, 40), 0.02),
+                                               (3, 130, 200, (7, 190), 0.05),
+                                               (4, 256, 256, (128, 128), 0.0)])
+def test_virtual_slabs_match_oracle(dymu, oracle, S, nx, ny, goal, frac):
+    F = oracle.synth_speed(nx, ny, seed=31, obst_frac=frac, obst_seed=5, goal=goal)
+    T, rounds = solve_virtual_slabs(dymu, F, goal, S)
+    Tref, _ = oracle.fmm(F, goal)
+    assert np.array_equal(np.isinf(T), np.isinf(Tref))
+    fin = np.isfinite(Tref)
+    assert (np.abs(T[fin] - Tref[fin]) / np.maximum(1, Tref[fin])).max() <= 1e-12
+    assert rounds > 1
