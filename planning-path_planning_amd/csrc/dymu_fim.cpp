@@ -29,7 +29,9 @@ struct dymu_ctx {
   dymu_opts opts{};
   int cu_count = 256;
 
-  int variant = 2;  // 1: 32x32 tile per workgroup, 2: 8x8 tile per wave (DYMU_KERNEL)
+  // 1: 32x32 tile per workgroup, 2: 8x8 tile per wave (Jacobi),
+  // 3: two 8x8 tiles per wave (red-black); DYMU_KERNEL overrides
+  int variant = 3;
 
   // tile workspace
   uint32_t tiles_cap = 0;
@@ -165,7 +167,8 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   a.shard_cap = ntiles;
   a.tile_epoch = c->d_tile_epoch;
   a.stats = c->d_stats;
-  D.blocks = c->opts.grid_blocks > 0 ? c->opts.grid_blocks : c->cu_count * 8;
+  // resident workgroups per CU at the kernels' register budgets (v3: 76 VGPRs -> 6 waves/SIMD)
+  D.blocks = c->opts.grid_blocks > 0 ? c->opts.grid_blocks : c->cu_count * (c->variant == 3 ? 6 : 8);
   D.live = true;
   return DYMU_OK;
 }
@@ -191,7 +194,9 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
       }
       HIPC(c, hipEventRecord(c->prof_ev[D.prof_used], st));
     }
-    HIPC(c, c->variant == 1 ? launch_pass(a, D.blocks, st) : launch_pass_w8(a, D.blocks, st));
+    HIPC(c, c->variant == 1   ? launch_pass(a, D.blocks, st)
+            : c->variant == 2 ? launch_pass_w8(a, D.blocks, st)
+                              : launch_pass_rb(a, D.blocks, st));
     if (prof) {
       HIPC(c, hipEventRecord(c->prof_ev[D.prof_used + 1], st));
       D.prof_used += 2;
@@ -349,7 +354,10 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
   }
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-  if (const char* kv = std::getenv("DYMU_KERNEL")) c->variant = std::atoi(kv) == 1 ? 1 : 2;
+  if (const char* kv = std::getenv("DYMU_KERNEL")) {
+    const int v = std::atoi(kv);
+    c->variant = (v >= 1 && v <= 3) ? v : 3;
+  }
   if (e == hipSuccess) e = hipMalloc(&c->d_counts, sizeof(uint32_t) * 4 * kShards);
   if (e == hipSuccess)
     e = hipMalloc(&c->d_stats, sizeof(unsigned long long) * kShards * kStatSlots);

@@ -46,6 +46,7 @@ hipError_t launch_seed(double* T, uint64_t ld, int64_t gi, int64_t gj, uint32_t*
                        int set_goal, hipStream_t st);
 hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st);        // v1: 32x32 tile / workgroup
 hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st);     // v2: 8x8 tile / wave
+hipError_t launch_pass_rb(const PassArgs& a, int blocks, hipStream_t st);     // v3: 2 x 8x8 tiles / wave, red-black
 hipError_t launch_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,
                                const double* new_lo, const double* new_hi, int ntx, int nty,
                                int tile_w, uint32_t* list, uint32_t* counts, uint32_t cap,

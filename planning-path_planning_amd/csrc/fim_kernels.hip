@@ -399,6 +399,212 @@ __global__ __launch_bounds__(256) void k_fim_pass_w8(PassArgs a) {
 }
 
 
+
+// ---------------------------------------------------------------------------
+// v3 pass kernel: red-black Gauss-Seidel, two 8x8 tiles per wave.
+// Half-wave h (lanes 32h..32h+31) owns one tile; lane (r = l>>2, q = l&3) owns
+// the two horizontally adjacent cells (r, 2q) and (r, 2q+1), one of each
+// checkerboard colour: red column 2q + (r&1), black column 2q + 1 - (r&1).
+// A sweep updates all red cells from the current image, then all black cells
+// from the freshly written reds (Gauss-Seidel on the two colours), so a sweep
+// moves information two cells for the cost of one Jacobi sweep of 64 lanes.
+// Everything else (halo ring, ballot convergence, edge flags, enqueue
+// aggregation) is as in v2.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool rb_update(double* img, int slot, double f, double& t) {
+  const double south = img[slot - (WT + 2)];
+  const double west = img[slot - 1];
+  const double east = img[slot + 1];
+  const double north = img[slot + (WT + 2)];
+  const double tx_ = minnn(west, east), ty_ = minnn(north, south);
+  if (minnn(tx_, ty_) + 0.7071 * f < t) {  // exact skip bound (see v2)
+    const double u = eikonal(tx_, ty_, f);  // :531-535
+    if (u < t) {                            // :537
+      t = u;
+      return true;
+    }
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(256) void k_fim_pass_rb(PassArgs a) {
+  __shared__ uint32_t s_q[QCAP];
+  __shared__ uint32_t s_pref[kShards + 1];
+  __shared__ uint32_t s_nq, s_base;
+  __shared__ unsigned long long s_visits, s_sweeps;
+  __shared__ double s_img[8][(WT + 2) * (WT + 2)];  // one 10x10 image per half-wave
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int half = lane >> 5;
+  const int hl = lane & 31;
+  const int r = hl >> 2, q = hl & 3;
+  const int cr = 2 * q + (r & 1), cb = 2 * q + 1 - (r & 1);  // red / black column
+  const uint32_t shard = blockIdx.x % kShards;
+
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int k = 0; k < kShards; ++k) {
+      s_pref[k] = acc;
+      acc += a.count_in[k];
+    }
+    s_pref[kShards] = acc;
+    s_nq = 0;
+    s_visits = 0;
+    s_sweeps = 0;
+  }
+  __syncthreads();
+  const uint32_t n_active = s_pref[kShards];
+  if (blockIdx.x == 0) {
+    if (tid < kShards) a.count_clear[tid] = 0u;
+    if (tid == 0 && n_active > 0) {
+      atomicAdd(&a.stats[kStatPasses], 1ull);
+      atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
+    }
+  }
+
+  unsigned long long my_visits = 0, my_sweeps = 0;
+  double* img = s_img[wv * 2 + half];
+  const int sr = (r + 1) * (WT + 2) + (cr + 1);  // red slot
+  const int sb = (r + 1) * (WT + 2) + (cb + 1);  // black slot
+  const unsigned long long hmask = half ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+  const uint32_t nslots = gridDim.x * 8u;  // tile slots: 4 waves x 2 halves per block
+  for (uint32_t base = (blockIdx.x * 4u + (uint32_t)wv) * 2u; base < n_active;
+       base += nslots) {
+    const uint32_t li = base + (uint32_t)half;
+    const bool has = li < n_active;  // the second half may have no tile
+    uint32_t tile = 0;
+    int tx = 0, ty = 0;
+    if (has) {
+      tile = list_at(a.list_in, a.shard_cap, s_pref, li);
+      tx = (int)(tile % (uint32_t)a.ntx);
+      ty = (int)(tile / (uint32_t)a.ntx);
+    }
+    const int64_t i0 = (int64_t)tx * WT, j0 = (int64_t)ty * WT;
+    const int64_t gj = j0 + r, gir = i0 + cr, gib = i0 + cb;
+    const bool rowin = has && gj < a.ny;
+    double tr = dinf(), fr = dinf(), tb = dinf(), fb = dinf();
+    if (rowin && gir < a.nx) {
+      tr = a.T[gj * a.ld + gir];
+      fr = a.F[gj * a.ld + gir];
+    }
+    if (rowin && gib < a.nx) {
+      tb = a.T[gj * a.ld + gib];
+      fb = a.F[gj * a.ld + gib];
+    }
+    // halo ring: west/east cells of row r (lanes q==0 / q==3), south/north
+    // cells of columns 2q, 2q+1 (lanes r==0 / r==7)
+    double hw = dinf(), he = dinf(), hs0 = dinf(), hs1 = dinf(), hn0 = dinf(), hn1 = dinf();
+    if (rowin) {
+      if (q == 0 && i0 > 0) hw = a.T[gj * a.ld + (i0 - 1)];
+      if (q == 3 && i0 + WT < a.nx) he = a.T[gj * a.ld + (i0 + WT)];
+    }
+    if (has) {
+      const int64_t c0 = i0 + 2 * q, c1 = c0 + 1;
+      if (r == 0 && (j0 > 0 || a.ghost_lo)) {
+        if (c0 < a.nx) hs0 = a.T[(j0 - 1) * a.ld + c0];
+        if (c1 < a.nx) hs1 = a.T[(j0 - 1) * a.ld + c1];
+      }
+      if (r == WT - 1) {
+        const int64_t jn = j0 + WT;
+        if (jn < a.ny || (jn == a.ny && a.ghost_hi)) {
+          if (c0 < a.nx) hn0 = a.T[jn * a.ld + c0];
+          if (c1 < a.nx) hn1 = a.T[jn * a.ld + c1];
+        }
+      }
+    }
+    {
+      const int row = (r + 1) * (WT + 2);
+      if (q == 0) img[row] = hw;
+      if (q == 3) img[row + WT + 1] = he;
+      if (r == 0) {
+        img[1 + 2 * q] = hs0;
+        img[2 + 2 * q] = hs1;
+      }
+      if (r == WT - 1) {
+        img[(WT + 1) * (WT + 2) + 1 + 2 * q] = hn0;
+        img[(WT + 1) * (WT + 2) + 2 + 2 * q] = hn1;
+      }
+      img[sb] = tb;
+    }
+    const double tr0 = tr, tb0 = tb;
+    int sweeps = 0;
+    bool capped = true;
+    while (sweeps < a.max_inner) {
+      __builtin_amdgcn_wave_barrier();
+      const bool ir = rb_update(img, sr, fr, tr);  // red from black
+      img[sr] = tr;
+      __builtin_amdgcn_wave_barrier();
+      const bool ib = rb_update(img, sb, fb, tb);  // black from fresh red
+      img[sb] = tb;
+      ++sweeps;
+      if (!__any(ir || ib)) {
+        capped = false;
+        break;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (has) {
+      my_visits += 1;
+      my_sweeps += (unsigned long long)sweeps;
+    }
+    const bool dr = tr < tr0, db = tb < tb0;
+    if (dr) a.T[gj * a.ld + gir] = tr;
+    if (db) a.T[gj * a.ld + gib] = tb;
+    // edge flags of this half's tile (cells on row 0 / 7, column 0 / 7)
+    const bool w_dec = (cr == 0 && dr) || (cb == 0 && db);
+    const bool e_dec = (cr == WT - 1 && dr) || (cb == WT - 1 && db);
+    const unsigned long long mS = __ballot(r == 0 && (dr || db)) & hmask;
+    const unsigned long long mN = __ballot(r == WT - 1 && (dr || db)) & hmask;
+    const unsigned long long mW = __ballot(w_dec) & hmask;
+    const unsigned long long mE = __ballot(e_dec) & hmask;
+    const unsigned long long mC = __ballot(capped && has) & hmask;
+    bool want = false;
+    int nx_t = tx, ny_t = ty;
+    if (has) {
+      if (hl == 0) { want = mS && ty > 0; ny_t = ty - 1; }
+      else if (hl == 1) { want = mW && tx > 0; nx_t = tx - 1; }
+      else if (hl == 2) { want = mE && tx + 1 < a.ntx; nx_t = tx + 1; }
+      else if (hl == 3) { want = mN && ty + 1 < a.nty; ny_t = ty + 1; }
+      else if (hl == 4) { want = mC != 0ull; }
+    }
+    if (want) {
+      const uint32_t nt = (uint32_t)ny_t * (uint32_t)a.ntx + (uint32_t)nx_t;
+      if (a.tile_epoch[nt] < a.epoch && atomicMax(&a.tile_epoch[nt], a.epoch) < a.epoch) {
+        const uint32_t pos = atomicAdd(&s_nq, 1u);
+        if (pos < QCAP) {
+          s_q[pos] = nt;
+        } else {
+          const uint32_t gp = atomicAdd(&a.count_out[shard], 1u);
+          a.list_out[(uint64_t)shard * a.shard_cap + gp] = nt;
+        }
+      }
+    }
+  }
+  if (lane == 0 && my_visits) {
+    atomicAdd(&s_visits, my_visits);
+    atomicAdd(&s_sweeps, my_sweeps);
+  }
+  if (lane == 32 && my_visits) {  // each half counted its own tiles
+    atomicAdd(&s_visits, my_visits);
+    atomicAdd(&s_sweeps, my_sweeps);
+  }
+  __syncthreads();
+  const uint32_t nq = s_nq < QCAP ? s_nq : QCAP;
+  if (tid == 0) {
+    if (nq) s_base = atomicAdd(&a.count_out[shard], nq);
+    if (s_visits) {
+      unsigned long long* st = a.stats + (uint64_t)shard * kStatSlots;
+      atomicAdd(&st[kStatVisits], s_visits);
+      atomicAdd(&st[kStatSweeps], s_sweeps);
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = tid; k < nq; k += blockDim.x)
+    a.list_out[(uint64_t)shard * a.shard_cap + s_base + k] = s_q[k];
+}
+
 // ---------------------------------------------------------------------------
 // Sharded (row-slab) mode: merge freshly received neighbour rows into the
 // ghost rows (values only decrease, so a min-merge) and seed the tiles of the
@@ -505,6 +711,11 @@ hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st) {
 
 hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st) {
   hipLaunchKernelGGL(k_fim_pass_w8, dim3(blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_pass_rb(const PassArgs& a, int blocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_fim_pass_rb, dim3(blocks), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

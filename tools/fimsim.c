@@ -41,6 +41,7 @@ static long long cell_updates;
 static long long subpasses, subvisits;
 static int SB = 8;
 static int PRUNE = 0;
+static int GROUP = 64;
 static double EPSR = 0;
 static long long hist[6];
 
@@ -235,6 +236,7 @@ int main(int argc, char** argv) {
   int CAP = argc > 7 ? atoi(argv[7]) : 0;
   PRUNE = argc > 8 ? atoi(argv[8]) : 0;
   EPSR = argc > 9 ? atof(argv[9]) : 0;
+  if (getenv("GROUP")) GROUP = atoi(getenv("GROUP"));
   long long group_cost = 0; int gmax = 0, gcnt = 0;
   double frac = 0.02;
   size_t n = (size_t)N * N;
@@ -283,7 +285,7 @@ int main(int argc, char** argv) {
       visits++;
       sweeps += sw;
       if (sw > gmax) gmax = sw;
-      if (++gcnt == 64) { group_cost += gmax; gmax = 0; gcnt = 0; }
+      if (++gcnt == GROUP) { group_cost += gmax; gmax = 0; gcnt = 0; }
       int cand[5], ncand = 0;
       if ((e & 1) && ty > 0) cand[ncand++] = t - ntx;
       if ((e & 2) && tx > 0) cand[ncand++] = t - 1;
@@ -309,7 +311,7 @@ int main(int argc, char** argv) {
     int* tmp = cur; cur = nxt; nxt = tmp; nc = nn;
   }
   printf("  visit max-rel-improvement histogram: new=%lld >1e-6=%lld >1e-10=%lld >1e-13=%lld >0=%lld none=%lld\n", hist[0], hist[1], hist[2], hist[3], hist[4], hist[5]);
-  printf("  lane-per-tile wave cost: %lld group-sweeps => %.1f sweeps per tile-visit (incl. max-over-64)\n", group_cost, 64.0 * group_cost / visits);
+  printf("  lane-per-tile wave cost: %lld group-sweeps => %.1f sweeps per tile-visit (incl. max-over-64)\n", group_cost, (double)GROUP * group_cost / visits);
   if (DELTA > 0) printf("  delta=%.1f deferred=%lld\n", DELTA, deferred);
   double sum = 0;
   for (size_t k = 0; k < n; k++) if (T[k] < INF) sum += T[k];
