@@ -131,6 +131,13 @@ int dymu_synth_speed(dymu_ctx* ctx, double* dF, uint32_t nx, uint32_t ny, uint64
                      uint64_t row0, uint64_t seed, double obst_frac, uint64_t obst_seed,
                      uint32_t goal_i, uint32_t goal_j, void* stream);
 
+/* Arithmetic self-test: out[k] = the kernels' Eikonal candidate for
+ * (Tx[k], Ty[k], C[k]) (reference :531-535), computed by the same device code
+ * the pass kernels use (fast = 1: the range-restricted correctly rounded sqrt).
+ * Device pointers; blocks until done. */
+int dymu_eikonal_batch(dymu_ctx* ctx, const double* tx, const double* ty, const double* c,
+                       double* out, uint64_t n, int fast);
+
 /* Device memory helpers (so a host without torch can run the device path). */
 int dymu_device_alloc(dymu_ctx* ctx, size_t bytes, void** dptr);
 int dymu_device_free(dymu_ctx* ctx, void* dptr);

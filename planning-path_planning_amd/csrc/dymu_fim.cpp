@@ -498,6 +498,15 @@ int dymu_slab_rows(uint32_t ny, uint32_t nranks, uint32_t rank, uint32_t* row0, 
   return DYMU_OK;
 }
 
+int dymu_eikonal_batch(dymu_ctx* c, const double* tx, const double* ty, const double* cc,
+                       double* out, uint64_t n, int fast) {
+  if (!c || !tx || !ty || !cc || !out) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  HIPC(c, launch_eikonal_batch(tx, ty, cc, out, n, fast, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return DYMU_OK;
+}
+
 int dymu_set_profiling(dymu_ctx* c, int on) {
   if (!c) return DYMU_ERR_ARG;
   c->profiling = on;

@@ -411,15 +411,62 @@ __global__ __launch_bounds__(256) void k_fim_pass_w8(PassArgs a) {
 // Everything else (halo ring, ballot convergence, edge flags, enqueue
 // aggregation) is as in v2.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool rb_update(double* img, int slot, double f, double& t) {
-  const double south = img[slot - (WT + 2)];
+// Image row pitch 12 doubles: the 32 red (or black) cells of a half-wave, and
+// every +-1 / +-pitch shift of them, fall on 32 distinct ds_read_b64 bank pairs
+// and 16 distinct ds_write_b64 banks per 16-lane group (pitch 10 was 2-way).
+constexpr int IP = 12;
+
+// v_min_f64 on operands that are never NaN (T >= 0 or +inf): one instruction,
+// no canonicalisation (the compiler cannot prove no-NaN for fmin).
+__device__ __forceinline__ double vmin64(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// Correctly rounded sqrt for x in [2^-767, 2^1023]: LLVM's f64 sqrt expansion
+// (rsq + Goldschmidt/Newton refinement) minus its range scaling and special-
+// value selects, which are identities on that range.  Bit-identical to sqrt()
+// there; x = 2C^2 - d^2 >= C^2 >= 2^-767 whenever C >= 2^-383 (kFastMinF).
+__device__ __forceinline__ double sqrt_cr_fast(double x) {
+  const double y0 = __builtin_amdgcn_rsq(x);
+  double s = x * y0;
+  double h = y0 * 0.5;
+  const double e = __builtin_fma(-h, s, 0.5);
+  s = __builtin_fma(s, e, s);
+  h = __builtin_fma(h, e, h);
+  double d = __builtin_fma(-s, s, x);
+  s = __builtin_fma(d, h, s);
+  d = __builtin_fma(-s, s, x);
+  s = __builtin_fma(d, h, s);
+  return s;
+}
+constexpr double kFastMinF = 0x1p-383;
+
+// One cell of the reference update (:504-537) against the image.  Preconditions
+// (guaranteed by the skip test): f finite and min(Tx,Ty) finite, so the
+// reference's "Tx < inf && Ty < inf" is implied by |Tx - Ty| < C.
+// c2x2 = 2*(C*C) is precomputed: the same two roundings as 2*pow(C,2.0).
+template <bool FAST>
+__device__ __forceinline__ bool rb_update(double* img, int slot, double f, double k1, double c2x2,
+                                          double& t) {
+  const double south = img[slot - IP];
   const double west = img[slot - 1];
   const double east = img[slot + 1];
-  const double north = img[slot + (WT + 2)];
-  const double tx_ = minnn(west, east), ty_ = minnn(north, south);
-  if (minnn(tx_, ty_) + 0.7071 * f < t) {  // exact skip bound (see v2)
-    const double u = eikonal(tx_, ty_, f);  // :531-535
-    if (u < t) {                            // :537
+  const double north = img[slot + IP];
+  const double tx_ = vmin64(west, east), ty_ = vmin64(north, south);
+  const double m = vmin64(tx_, ty_);
+  if (m + k1 < t) {  // exact skip bound U >= min + C/sqrt(2); k1 = 0.7071*C
+    const double dd = tx_ - ty_;
+    double u;
+    if (fabs(dd) < f) {
+      const double r = c2x2 - dd * dd;
+      const double sq = FAST ? sqrt_cr_fast(r) : sqrt(r);
+      u = ((tx_ + ty_) + sq) * 0.5;  // (Tx + Ty + sqrt(...)) / 2, /2 exact
+    } else {
+      u = m + f;  // fmin(Tx,Ty) + C
+    }
+    if (u < t) {  // :537
       t = u;
       return true;
     }
@@ -427,12 +474,59 @@ __device__ __forceinline__ bool rb_update(double* img, int slot, double f, doubl
   return false;
 }
 
+// The update of rb_update without the skip test, for the arithmetic self-test
+// (dymu_eikonal_batch): candidate T' from (Tx, Ty, C) as at :531-535.
+template <bool FAST>
+__device__ __forceinline__ double update_value(double tx_, double ty_, double f) {
+  const double m = minnn(tx_, ty_);
+  if (!(f < dinf()) || !(m < dinf())) return m + f;  // outside the kernel's fast path
+  const double dd = tx_ - ty_;
+  if (fabs(dd) < f) {
+    const double r = 2.0 * (f * f) - dd * dd;
+    const double sq = FAST ? sqrt_cr_fast(r) : sqrt(r);
+    return ((tx_ + ty_) + sq) * 0.5;
+  }
+  return m + f;
+}
+
+template <bool FAST>
+__global__ void k_eikonal_batch(const double* tx, const double* ty, const double* c, double* out,
+                                uint64_t n) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+       k += (uint64_t)gridDim.x * blockDim.x)
+    out[k] = update_value<FAST>(tx[k], ty[k], c[k]);
+}
+
+template <bool FAST>
+__device__ __forceinline__ int rb_sweeps(double* img, int sr, int sb, double fr, double fb,
+                                         double& tr, double& tb, int max_inner, bool& capped) {
+  const double k1r = 0.7071 * fr, k1b = 0.7071 * fb;
+  const double c2r = 2.0 * (fr * fr), c2b = 2.0 * (fb * fb);
+  int sweeps = 0;
+  capped = true;
+  while (sweeps < max_inner) {
+    __builtin_amdgcn_wave_barrier();
+    const bool ir = rb_update<FAST>(img, sr, fr, k1r, c2r, tr);  // red from black
+    img[sr] = tr;
+    __builtin_amdgcn_wave_barrier();
+    const bool ib = rb_update<FAST>(img, sb, fb, k1b, c2b, tb);  // black from fresh red
+    img[sb] = tb;
+    ++sweeps;
+    if (!__any(ir || ib)) {
+      capped = false;
+      break;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  return sweeps;
+}
+
 __global__ __launch_bounds__(256) void k_fim_pass_rb(PassArgs a) {
   __shared__ uint32_t s_q[QCAP];
   __shared__ uint32_t s_pref[kShards + 1];
   __shared__ uint32_t s_nq, s_base;
   __shared__ unsigned long long s_visits, s_sweeps;
-  __shared__ double s_img[8][(WT + 2) * (WT + 2)];  // one 10x10 image per half-wave
+  __shared__ double s_img[8][(WT + 2) * IP];  // one 10-row image (pitch IP) per half-wave
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -466,8 +560,8 @@ __global__ __launch_bounds__(256) void k_fim_pass_rb(PassArgs a) {
 
   unsigned long long my_visits = 0, my_sweeps = 0;
   double* img = s_img[wv * 2 + half];
-  const int sr = (r + 1) * (WT + 2) + (cr + 1);  // red slot
-  const int sb = (r + 1) * (WT + 2) + (cb + 1);  // black slot
+  const int sr = (r + 1) * IP + (cr + 1);  // red slot
+  const int sb = (r + 1) * IP + (cb + 1);  // black slot
   const unsigned long long hmask = half ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
   const uint32_t nslots = gridDim.x * 8u;  // tile slots: 4 waves x 2 halves per block
   for (uint32_t base = (blockIdx.x * 4u + (uint32_t)wv) * 2u; base < n_active;
@@ -515,7 +609,7 @@ __global__ __launch_bounds__(256) void k_fim_pass_rb(PassArgs a) {
       }
     }
     {
-      const int row = (r + 1) * (WT + 2);
+      const int row = (r + 1) * IP;
       if (q == 0) img[row] = hw;
       if (q == 3) img[row + WT + 1] = he;
       if (r == 0) {
@@ -523,28 +617,17 @@ __global__ __launch_bounds__(256) void k_fim_pass_rb(PassArgs a) {
         img[2 + 2 * q] = hs1;
       }
       if (r == WT - 1) {
-        img[(WT + 1) * (WT + 2) + 1 + 2 * q] = hn0;
-        img[(WT + 1) * (WT + 2) + 2 + 2 * q] = hn1;
+        img[(WT + 1) * IP + 1 + 2 * q] = hn0;
+        img[(WT + 1) * IP + 2 + 2 * q] = hn1;
       }
       img[sb] = tb;
     }
     const double tr0 = tr, tb0 = tb;
-    int sweeps = 0;
-    bool capped = true;
-    while (sweeps < a.max_inner) {
-      __builtin_amdgcn_wave_barrier();
-      const bool ir = rb_update(img, sr, fr, tr);  // red from black
-      img[sr] = tr;
-      __builtin_amdgcn_wave_barrier();
-      const bool ib = rb_update(img, sb, fb, tb);  // black from fresh red
-      img[sb] = tb;
-      ++sweeps;
-      if (!__any(ir || ib)) {
-        capped = false;
-        break;
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
+    // sqrt without range scaling is exact while every finite C >= 2^-383
+    const bool fast = __all(!(fr < kFastMinF) && !(fb < kFastMinF));
+    bool capped;
+    const int sweeps = fast ? rb_sweeps<true>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped)
+                            : rb_sweeps<false>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped);
     if (has) {
       my_visits += 1;
       my_sweeps += (unsigned long long)sweeps;
@@ -716,6 +799,20 @@ hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st) {
 
 hipError_t launch_pass_rb(const PassArgs& a, int blocks, hipStream_t st) {
   hipLaunchKernelGGL(k_fim_pass_rb, dim3(blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_eikonal_batch(const double* tx, const double* ty, const double* c, double* out,
+                                uint64_t n, int fast, hipStream_t st) {
+  uint64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks == 0) return hipSuccess;
+  if (fast)
+    hipLaunchKernelGGL(k_eikonal_batch<true>, dim3((unsigned)blocks), dim3(256), 0, st, tx, ty, c,
+                       out, n);
+  else
+    hipLaunchKernelGGL(k_eikonal_batch<false>, dim3((unsigned)blocks), dim3(256), 0, st, tx, ty,
+                       c, out, n);
   return hipGetLastError();
 }
 

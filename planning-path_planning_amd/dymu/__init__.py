@@ -95,6 +95,7 @@ FIM_SYMBOLS = {
     "dymu_memcpy_d2h": (_i32, [_vp, _vp, _vp, ctypes.c_size_t]),
     "dymu_memcpy_h2d": (_i32, [_vp, _vp, _vp, ctypes.c_size_t]),
     "dymu_set_profiling": (_i32, [_vp, _i32]),
+    "dymu_eikonal_batch": (_i32, [_vp, _vp, _vp, _vp, _vp, _u64, _i32]),
     "dymu_slab_rows": (_i32, [_u32, _u32, _u32, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
     "dymu_dom_begin": (_i32, [_vp, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, _vp]),
     "dymu_dom_run": (_i32, [_vp, _u32, _vp]),
@@ -244,6 +245,24 @@ class Engine:
         st = DymuStats()
         _check(self._lib.dymu_dom_finish(self.ctx, stream or None, ctypes.byref(st)), self.ctx)
         return st.as_dict()
+
+    def eikonal_batch(self, tx: np.ndarray, ty: np.ndarray, c: np.ndarray,
+                      fast: bool = True) -> np.ndarray:
+        """The kernels' update arithmetic on the GPU (bit-level self-test)."""
+        arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (tx, ty, c)]
+        n = arrs[0].size
+        ptrs = [self.alloc(8 * n) for _ in range(4)]
+        try:
+            for p, a in zip(ptrs, arrs):
+                self.h2d(p, a)
+            _check(self._lib.dymu_eikonal_batch(self.ctx, ptrs[0], ptrs[1], ptrs[2], ptrs[3], n,
+                                                1 if fast else 0), self.ctx)
+            out = np.empty(n)
+            self.d2h(out, ptrs[3])
+            return out
+        finally:
+            for p in ptrs:
+                self.free(p)
 
     def set_profiling(self, on: bool):
         _check(self._lib.dymu_set_profiling(self.ctx, 1 if on else 0), self.ctx)
