@@ -137,12 +137,24 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 6),
             "traffic": None,
-            "kernel": "k_fim_pass",
+            "kernel": "k_fim_pass_rb",
             "bytes_per_launch": bytes_alg / kern_n,
             "avg_launch_us": kern_ms * 1e3 / kern_n,
             "per_unit": "24 B per cell-visit (SURVEY s8(d)(ii))",
             "headline_solve_GBs": round(N * N * BYTES_PER_CELL_SOLVE * K / dt / 1e9, 3),
         }
+    if roof is not None:
+        # HBM bytes per launch from the PMC counters of the same kernel and
+        # workload (tools/pmc_round.sh -> tools/pmc_summary.py), if committed
+        import glob
+        pm = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+        if pm:
+            d = json.load(open(pm[-1]))
+            if d.get("kernel") and roof["kernel"] in d["kernel"]:
+                roof["traffic"] = round(d["traffic_bytes_per_launch"] / 1e6, 3)
+                roof["traffic_unit"] = "MB per launch (PMC, FETCH x2 corrected)"
+                roof["traffic_source"] = os.path.basename(pm[-1])
+                roof["bytes_per_launch_MB"] = round(roof.pop("bytes_per_launch") / 1e6, 3)
     line = {
         "metric": "global total-cost-map Mcells/s (16384^2 grid); iters to converge",
         "value": round(value, 3),

@@ -186,21 +186,20 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
     a.count_out = D.counts[(p + 1) % 3];
     a.count_clear = D.counts[(p + 2) % 3];
     a.epoch = D.eb + (uint32_t)p + 2u;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
     if (prof) {
       while (c->prof_ev.size() < D.prof_used + 2) {
         hipEvent_t e;
         HIPC(c, hipEventCreate(&e));
         c->prof_ev.push_back(e);
       }
-      HIPC(c, hipEventRecord(c->prof_ev[D.prof_used], st));
-    }
-    HIPC(c, c->variant == 1   ? launch_pass(a, D.blocks, st)
-            : c->variant == 2 ? launch_pass_w8(a, D.blocks, st)
-                              : launch_pass_rb(a, D.blocks, st));
-    if (prof) {
-      HIPC(c, hipEventRecord(c->prof_ev[D.prof_used + 1], st));
+      e0 = c->prof_ev[D.prof_used];
+      e1 = c->prof_ev[D.prof_used + 1];
       D.prof_used += 2;
     }
+    HIPC(c, c->variant == 1   ? launch_pass(a, D.blocks, st, e0, e1)
+            : c->variant == 2 ? launch_pass_w8(a, D.blocks, st, e0, e1)
+                              : launch_pass_rb(a, D.blocks, st, e0, e1));
     ++D.launches;
   }
   return DYMU_OK;

@@ -44,9 +44,12 @@ hipError_t launch_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, 
 hipError_t launch_seed(double* T, uint64_t ld, int64_t gi, int64_t gj, uint32_t* list,
                        uint32_t* count, uint32_t* tile_epoch, uint32_t epoch, uint32_t tile,
                        int set_goal, hipStream_t st);
-hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st);        // v1: 32x32 tile / workgroup
-hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st);     // v2: 8x8 tile / wave
-hipError_t launch_pass_rb(const PassArgs& a, int blocks, hipStream_t st);     // v3: 2 x 8x8 tiles / wave, red-black
+hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st,
+                      hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);        // v1: 32x32 tile / workgroup
+hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st,
+                      hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);     // v2: 8x8 tile / wave
+hipError_t launch_pass_rb(const PassArgs& a, int blocks, hipStream_t st,
+                      hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);     // v3: 2 x 8x8 tiles / wave, red-black
 hipError_t launch_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,
                                const double* new_lo, const double* new_hi, int ntx, int nty,
                                int tile_w, uint32_t* list, uint32_t* counts, uint32_t cap,

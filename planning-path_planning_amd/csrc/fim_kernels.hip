@@ -12,6 +12,7 @@
 // neighbour tiles whose shared edge changed.  Values only decrease, every
 // update is the reference's exact arithmetic, so the converged map is the
 // fixed point the reference FMM reaches.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -787,18 +788,27 @@ hipError_t launch_seed(double* T, uint64_t ld, int64_t gi, int64_t gj, uint32_t*
   return hipGetLastError();
 }
 
-hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st) {
-  hipLaunchKernelGGL(k_fim_pass, dim3(blocks), dim3(256), 0, st, a);
+hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  if (e0 || e1)  // timestamps taken by the dispatch itself (no extra stream packets)
+    hipExtLaunchKernelGGL(k_fim_pass, dim3(blocks), dim3(256), 0, st, e0, e1, 0, a);
+  else
+    hipLaunchKernelGGL(k_fim_pass, dim3(blocks), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
-hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st) {
-  hipLaunchKernelGGL(k_fim_pass_w8, dim3(blocks), dim3(256), 0, st, a);
+hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  if (e0 || e1)  // timestamps taken by the dispatch itself (no extra stream packets)
+    hipExtLaunchKernelGGL(k_fim_pass_w8, dim3(blocks), dim3(256), 0, st, e0, e1, 0, a);
+  else
+    hipLaunchKernelGGL(k_fim_pass_w8, dim3(blocks), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
-hipError_t launch_pass_rb(const PassArgs& a, int blocks, hipStream_t st) {
-  hipLaunchKernelGGL(k_fim_pass_rb, dim3(blocks), dim3(256), 0, st, a);
+hipError_t launch_pass_rb(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  if (e0 || e1)  // timestamps taken by the dispatch itself (no extra stream packets)
+    hipExtLaunchKernelGGL(k_fim_pass_rb, dim3(blocks), dim3(256), 0, st, e0, e1, 0, a);
+  else
+    hipLaunchKernelGGL(k_fim_pass_rb, dim3(blocks), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
