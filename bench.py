@@ -72,6 +72,9 @@ def cpu_baseline(n_edge, obst):
     }
 
 
+KERNEL_NAMES = {1: "k_fim_pass", 2: "k_fim_pass_w8", 3: "k_fim_pass_rb", 4: "k_fim_pass_prio"}
+
+
 def run_single(args):
     import dymu
 
@@ -137,7 +140,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 6),
             "traffic": None,
-            "kernel": "k_fim_pass_rb",
+            "kernel": KERNEL_NAMES.get(st.get("kernel", 3), "k_fim_pass_rb"),
             "bytes_per_launch": bytes_alg / kern_n,
             "avg_launch_us": kern_ms * 1e3 / kern_n,
             "per_unit": "24 B per cell-visit (SURVEY s8(d)(ii))",
@@ -177,6 +180,7 @@ def main():
             "passes_per_solve": tot["passes"] / K,
             "tile_visits_per_solve": tot["tile_visits"] / K,
             "inner_sweeps_per_solve": tot["inner_sweeps"] / K,
+            "pass_kernel": st.get("kernel"),
         },
         "roofline": roof,
         "cpu_baseline": None,

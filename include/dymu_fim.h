@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define DYMU_ABI_VERSION 1
+#define DYMU_ABI_VERSION 2
 
 typedef enum dymu_status {
   DYMU_OK = 0,
@@ -55,6 +55,9 @@ typedef struct dymu_opts {
   int max_passes;       /* safety cap on FIM passes; 0 = derived from the grid size */
   int max_inner;        /* cap on in-tile sweeps per tile visit; 0 = default */
   int grid_blocks;      /* workgroups per pass launch; 0 = derived from the device */
+  int kernel;           /* pass kernel: 0 = auto (by grid size), 3 = plain block FIM,
+                           4 = priority passes */
+  int prio_target;      /* kernel 4: tiles relaxed per pass; 0 = default (64 per CU) */
 } dymu_opts;
 
 typedef struct dymu_stats {
@@ -66,6 +69,8 @@ typedef struct dymu_stats {
   uint64_t rounds;       /* sharded solver: halo-exchange rounds (0 single GPU) */
   double ms;             /* device time of the solve (HIP events), ms */
   int tile_w, tile_h;    /* tile geometry used */
+  int kernel;            /* pass kernel that ran (see dymu_opts.kernel) */
+  int reserved;
 } dymu_stats;
 
 /* Context: owns a HIP stream, events and workspace on one device. */

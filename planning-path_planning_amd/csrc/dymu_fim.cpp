@@ -30,8 +30,17 @@ struct dymu_ctx {
   int cu_count = 256;
 
   // 1: 32x32 tile per workgroup, 2: 8x8 tile per wave (Jacobi),
-  // 3: two 8x8 tiles per wave (red-black); DYMU_KERNEL overrides
-  int variant = 3;
+  // 3: two 8x8 tiles per wave (red-black), 4: v3 body + priority passes;
+  // 0 (default): per domain, 4 from prio_min_tiles 8x8 tiles up, else 3.
+  // DYMU_KERNEL overrides
+  int variant = 0;
+  uint32_t prio_min_tiles = 1u << 19;  // DYMU_PRIO_MIN_TILES
+  uint32_t prio_target = 0;  // v4: tiles relaxed per pass (DYMU_PRIO_TARGET)
+  double prio_kappa = 0.5;   // v4: histogram bin width / mean F (DYMU_PRIO_KAPPA)
+  float prio_frac = 0.0f;    // v4: ... or this fraction of the active list (DYMU_PRIO_FRAC)
+  int prio_trace = -1;       // v4: stamp phases of this pass index (DYMU_PRIO_TRACE)
+  unsigned long long* d_trace = nullptr;
+  int prio_debug = 0;        // v4: print the state after the first N passes (DYMU_PRIO_DEBUG)
 
   // tile workspace
   uint32_t tiles_cap = 0;
@@ -39,6 +48,12 @@ struct dymu_ctx {
   uint32_t* d_counts = nullptr;      // 3 x kShards words, own block
   uint32_t* d_tile_epoch = nullptr;  // tiles_cap
   unsigned long long* d_stats = nullptr;  // kStatSlots
+  // v4 priority state: keys 3 x tiles_cap, hist 3 x kShards x kBins,
+  // prio = {minkey[3] (u64), base[3] (f64), delta (f64)}
+  unsigned long long* d_keys = nullptr;
+  uint32_t keys_cap = 0;
+  uint32_t* d_hist = nullptr;
+  unsigned long long* d_prio = nullptr;
   uint32_t epoch_base = 0;
   uint32_t* h_count = nullptr;  // pinned
 
@@ -50,6 +65,7 @@ struct dymu_ctx {
   // current domain (whole grid or one row slab) being solved
   struct Dom {
     bool live = false;
+    int variant = 3;
     PassArgs a{};
     uint32_t ntiles = 0;
     uint32_t eb = 0;
@@ -103,6 +119,18 @@ int ensure_tiles(dymu_ctx* c, uint32_t ntiles) {
   return DYMU_OK;
 }
 
+int ensure_prio(dymu_ctx* c, uint32_t ntiles) {
+  if (!c->d_hist) HIPC(c, hipMalloc(&c->d_hist, sizeof(uint32_t) * 3 * kShards * kBins));
+  if (!c->d_prio) HIPC(c, hipMalloc(&c->d_prio, sizeof(unsigned long long) * 8));
+  if (ntiles <= c->keys_cap) return DYMU_OK;
+  if (c->d_keys) (void)hipFree(c->d_keys);
+  c->d_keys = nullptr;
+  c->keys_cap = 0;
+  HIPC(c, hipMalloc(&c->d_keys, sizeof(unsigned long long) * 3ull * ntiles));
+  c->keys_cap = ntiles;
+  return DYMU_OK;
+}
+
 int ensure_cells(dymu_ctx* c, uint64_t cells) {
   if (cells <= c->cells_cap) return DYMU_OK;
   if (c->d_F) (void)hipFree(c->d_F);
@@ -115,14 +143,28 @@ int ensure_cells(dymu_ctx* c, uint64_t cells) {
   return DYMU_OK;
 }
 
-int tile_w(const dymu_ctx* c) { return c->variant == 1 ? kTileW : kWaveTile; }
-int tile_h(const dymu_ctx* c) { return c->variant == 1 ? kTileH : kWaveTile; }
+double* prio_delta(dymu_ctx* c) { return reinterpret_cast<double*>(c->d_prio + 6); }
+double* prio_base(dymu_ctx* c, uint64_t q) { return reinterpret_cast<double*>(c->d_prio + 3 + q); }
+unsigned long long* prio_minkey(dymu_ctx* c, uint64_t q) { return c->d_prio + q; }
+uint32_t* prio_hist(dymu_ctx* c, uint64_t q) { return c->d_hist + q * kShards * kBins; }
+unsigned long long* prio_keys(dymu_ctx* c, uint64_t q) {
+  return c->d_keys + q * (uint64_t)c->dom.ntiles;
+}
+
+int tile_w(int variant) { return variant == 1 ? kTileW : kWaveTile; }
+int tile_h(int variant) { return variant == 1 ? kTileH : kWaveTile; }
 
 // ---- domain primitives (whole grid, or one row slab with ghost rows) ----
 int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t nrows, uint64_t ld,
               int ghost_lo, int ghost_hi, int64_t gi, int64_t gj, hipStream_t st) {
   if (!dF || !dT || nx == 0 || nrows == 0 || ld < nx) return DYMU_ERR_ARG;
-  const int TWd = tile_w(c), THd = tile_h(c);
+  int variant = c->variant;
+  if (variant == 0) {
+    const uint64_t t8 = (uint64_t)((nx + kWaveTile - 1) / kWaveTile) *
+                        (uint64_t)((nrows + kWaveTile - 1) / kWaveTile);
+    variant = t8 >= c->prio_min_tiles ? 4 : 3;
+  }
+  const int TWd = tile_w(variant), THd = tile_h(variant);
   if (ghost_hi && (nrows % (uint32_t)THd) != 0) return DYMU_ERR_ARG;
   if (gj >= 0 && (gi < 0 || gi >= (int64_t)nx || gj >= (int64_t)nrows)) return DYMU_ERR_ARG;
   const uint32_t ntx = (uint32_t)((nx + TWd - 1) / TWd), nty = (uint32_t)((nrows + THd - 1) / THd);
@@ -131,8 +173,10 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   const uint32_t ntiles = (uint32_t)ntiles64;
   int rc = ensure_tiles(c, ntiles);
   if (rc) return rc;
+  if (variant == 4 && (rc = ensure_prio(c, ntiles)) != DYMU_OK) return rc;
   auto& D = c->dom;
   D = dymu_ctx::Dom{};
+  D.variant = variant;
   D.ntiles = ntiles;
   D.max_passes = c->opts.max_passes > 0 ? (uint64_t)c->opts.max_passes : 4ull * ntiles + 1024ull;
   if ((uint64_t)c->epoch_base + D.max_passes + 8 >= 0xFFFFFFF0ull) {
@@ -148,12 +192,23 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   HIPC(c, hipMemsetAsync(c->d_counts, 0, sizeof(uint32_t) * 3 * kShards, st));
   HIPC(c, hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * kShards * kStatSlots, st));
   HIPC(c, launch_fill_inf(dT, ld, nx, ghost_lo ? -1 : 0, (int64_t)nrows + (ghost_hi ? 1 : 0), st));
+  PassArgs& a = D.a;
+  if (D.variant == 4) {
+    HIPC(c, launch_prio_init(dF, (int64_t)ld, nx, nrows, c->d_keys, 3ull * ntiles, c->d_hist,
+                             3ull * kShards * kBins, c->d_prio,
+                             reinterpret_cast<double*>(c->d_prio + 3), prio_delta(c), c->prio_kappa,
+                             st));
+    a.target = c->prio_target;
+    a.target_frac = c->prio_frac;
+    a.delta = prio_delta(c);
+  }
   if (gj >= 0) {
     const uint32_t gtile = (uint32_t)(gj / THd) * ntx + (uint32_t)(gi / TWd);
     HIPC(c, launch_seed(dT, ld, gi, gj, D.lists[0], D.counts[0], c->d_tile_epoch, D.eb + 1, gtile,
                         1, st));
+    if (D.variant == 4)
+      HIPC(c, launch_prio_seed(c->d_keys, c->d_hist, c->d_prio, gtile, 0.0, st));
   }
-  PassArgs& a = D.a;
   a.F = dF;
   a.T = dT;
   a.ld = (int64_t)ld;
@@ -164,11 +219,13 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   a.ghost_lo = ghost_lo;
   a.ghost_hi = ghost_hi;
   a.max_inner = c->opts.max_inner > 0 ? c->opts.max_inner : 4 * (TWd + THd);
+  if (const char* kv = std::getenv("DYMU_MAX_INNER")) a.max_inner = std::max(1, std::atoi(kv));
   a.shard_cap = ntiles;
   a.tile_epoch = c->d_tile_epoch;
   a.stats = c->d_stats;
   // resident workgroups per CU at the kernels' register budgets (v3: 76 VGPRs -> 6 waves/SIMD)
-  D.blocks = c->opts.grid_blocks > 0 ? c->opts.grid_blocks : c->cu_count * (c->variant == 3 ? 6 : 8);
+  D.blocks = c->opts.grid_blocks > 0 ? c->opts.grid_blocks
+                                      : c->cu_count * (D.variant == 4 ? 5 : D.variant == 3 ? 6 : 8);
   D.live = true;
   return DYMU_OK;
 }
@@ -186,6 +243,25 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
     a.count_out = D.counts[(p + 1) % 3];
     a.count_clear = D.counts[(p + 2) % 3];
     a.epoch = D.eb + (uint32_t)p + 2u;
+    if (D.variant == 4) {
+      a.key_in = prio_keys(c, p % 3);
+      a.key_out = prio_keys(c, (p + 1) % 3);
+      a.hist_in = prio_hist(c, p % 3);
+      a.hist_out = prio_hist(c, (p + 1) % 3);
+      a.hist_clear = prio_hist(c, (p + 2) % 3);
+      a.minkey_in = prio_minkey(c, p % 3);
+      a.minkey_out = prio_minkey(c, (p + 1) % 3);
+      a.minkey_clear = prio_minkey(c, (p + 2) % 3);
+      a.base_in = prio_base(c, p % 3);
+      a.base_out = prio_base(c, (p + 1) % 3);
+    }
+    const bool tr = D.variant == 4 && c->prio_trace >= 0 && p == (uint64_t)c->prio_trace;
+    if (tr) {
+      if (!c->d_trace)
+        HIPC(c, hipMalloc(&c->d_trace, sizeof(unsigned long long) * kTracePts * 65536));
+      HIPC(c, hipMemsetAsync(c->d_trace, 0, sizeof(unsigned long long) * kTracePts * D.blocks, st));
+      a.trace = c->d_trace;
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (prof) {
       while (c->prof_ev.size() < D.prof_used + 2) {
@@ -197,10 +273,48 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
       e1 = c->prof_ev[D.prof_used + 1];
       D.prof_used += 2;
     }
-    HIPC(c, c->variant == 1   ? launch_pass(a, D.blocks, st, e0, e1)
-            : c->variant == 2 ? launch_pass_w8(a, D.blocks, st, e0, e1)
+    HIPC(c, D.variant == 1   ? launch_pass(a, D.blocks, st, e0, e1)
+            : D.variant == 2 ? launch_pass_w8(a, D.blocks, st, e0, e1)
+            : D.variant == 4 ? launch_pass_prio(a, D.blocks, st, e0, e1)
                               : launch_pass_rb(a, D.blocks, st, e0, e1));
     ++D.launches;
+    if (tr) {
+      a.trace = nullptr;
+      std::vector<unsigned long long> h((size_t)kTracePts * D.blocks);
+      HIPC(c, hipStreamSynchronize(st));
+      HIPC(c, hipMemcpy(h.data(), c->d_trace, sizeof(unsigned long long) * h.size(),
+                        hipMemcpyDeviceToHost));
+      unsigned long long t0 = ~0ull;
+      for (int b = 0; b < D.blocks; ++b) t0 = std::min(t0, h[(size_t)b * kTracePts]);
+      std::fprintf(stderr, "TRACE pass %llu blocks %d (10ns ticks rel. first start)\n",
+                   (unsigned long long)p, D.blocks);
+      for (int b = 0; b < D.blocks; ++b) {
+        const unsigned long long* t = &h[(size_t)b * kTracePts];
+        auto rel = [&](int k) { return t[k] ? (long long)(t[k] - t0) : -1ll; };
+        std::fprintf(stderr, "B %d %lld %lld %lld %lld %lld %llu %llu %lld %lld %lld\n", b, rel(0),
+                     rel(1), rel(2), rel(3), rel(4), t[5] >> 32, t[5] & 0xffffffffull, rel(6),
+                     rel(7), rel(8));
+      }
+    }
+    if (D.variant == 4 && c->prio_debug && p < (uint64_t)c->prio_debug) {
+      unsigned long long pr[8];
+      uint32_t h[kShards * kBins], cnt[kShards];
+      HIPC(c, hipStreamSynchronize(st));
+      HIPC(c, hipMemcpy(pr, c->d_prio, sizeof pr, hipMemcpyDeviceToHost));
+      HIPC(c, hipMemcpy(h, prio_hist(c, (p + 1) % 3), sizeof h, hipMemcpyDeviceToHost));
+      HIPC(c, hipMemcpy(cnt, D.counts[(p + 1) % 3], sizeof cnt, hipMemcpyDeviceToHost));
+      double dd[4];
+      std::memcpy(dd, pr + 3, sizeof dd);
+      uint32_t n = 0, hs[kBins] = {0};
+      for (int q = 0; q < kShards; ++q) n += cnt[q];
+      for (int q = 0; q < kShards * kBins; ++q) hs[q % kBins] += h[q];
+      double mk[3];
+      std::memcpy(mk, pr, sizeof mk);
+      std::fprintf(stderr, "pass %llu n_out %u minkey %g %g %g base %g %g %g delta %g hist:",
+                   (unsigned long long)p, n, mk[0], mk[1], mk[2], dd[0], dd[1], dd[2], dd[3]);
+      for (int b = 0; b < kBins; ++b) if (hs[b]) std::fprintf(stderr, " %d:%u", b, hs[b]);
+      std::fprintf(stderr, "\n");
+    }
   }
   return DYMU_OK;
 }
@@ -225,8 +339,13 @@ int dom_merge(dymu_ctx* c, const double* lo, const double* hi, int32_t* d_pendin
   const uint64_t p = D.p;
   if (lo || hi)
     HIPC(c, launch_merge_ghosts(D.a.T, D.a.ld, D.a.nx, D.a.ny, lo, hi, D.a.ntx, D.a.nty,
-                                tile_w(c), D.lists[p % 3], D.counts[p % 3], D.ntiles,
-                                c->d_tile_epoch, D.eb + (uint32_t)p + 1u, st));
+                                tile_w(D.variant), D.lists[p % 3], D.counts[p % 3], D.ntiles,
+                                c->d_tile_epoch, D.eb + (uint32_t)p + 1u,
+                                D.variant == 4 ? prio_keys(c, p % 3) : nullptr,
+                                D.variant == 4 ? prio_hist(c, p % 3) : nullptr,
+                                D.variant == 4 ? prio_minkey(c, p % 3) : nullptr,
+                                D.variant == 4 ? prio_base(c, p % 3) : nullptr,
+                                D.variant == 4 ? prio_delta(c) : nullptr, st));
   if (d_pending) HIPC(c, launch_sum_counts(D.counts[p % 3], d_pending, st));
   return DYMU_OK;
 }
@@ -261,8 +380,9 @@ int dom_finish(dymu_ctx* c, hipStream_t st, dymu_stats* stats, double ms) {
     stats->max_active = h[kStatMaxActive];
     stats->rounds = 0;
     stats->ms = ms;
-    stats->tile_w = tile_w(c);
-    stats->tile_h = tile_h(c);
+    stats->tile_w = tile_w(D.variant);
+    stats->tile_h = tile_h(D.variant);
+    stats->kernel = D.variant;
   }
   D.live = false;
   return DYMU_OK;
@@ -353,9 +473,26 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
   }
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-  if (const char* kv = std::getenv("DYMU_KERNEL")) {
+  if (c->opts.kernel < 0 || c->opts.kernel > 4 || c->opts.prio_target < 0) {
+    dymu_destroy(c);
+    return DYMU_ERR_ARG;
+  }
+  c->variant = c->opts.kernel;
+  if (const char* kv = std::getenv("DYMU_KERNEL")) {  // development override
     const int v = std::atoi(kv);
-    c->variant = (v >= 1 && v <= 3) ? v : 3;
+    c->variant = (v >= 0 && v <= 4) ? v : 0;
+  }
+  if (e == hipSuccess) {
+    c->prio_target = c->opts.prio_target > 0 ? (uint32_t)c->opts.prio_target
+                                             : (uint32_t)c->cu_count * 64u;
+    if (const char* kv = std::getenv("DYMU_PRIO_TARGET")) c->prio_target = (uint32_t)std::atol(kv);
+    if (const char* kv = std::getenv("DYMU_PRIO_KAPPA")) c->prio_kappa = std::atof(kv);
+    if (!(c->prio_kappa > 0.0)) c->prio_kappa = 0.5;
+    if (const char* kv = std::getenv("DYMU_PRIO_MIN_TILES"))
+      c->prio_min_tiles = (uint32_t)std::atol(kv);
+    if (const char* kv = std::getenv("DYMU_PRIO_FRAC")) c->prio_frac = (float)std::atof(kv);
+    if (const char* kv = std::getenv("DYMU_PRIO_TRACE")) c->prio_trace = std::atoi(kv);
+    if (const char* kv = std::getenv("DYMU_PRIO_DEBUG")) c->prio_debug = std::atoi(kv);
   }
   if (e == hipSuccess) e = hipMalloc(&c->d_counts, sizeof(uint32_t) * 4 * kShards);
   if (e == hipSuccess)
@@ -379,6 +516,10 @@ int dymu_destroy(dymu_ctx* c) {
   if (c->d_lists) (void)hipFree(c->d_lists);
   if (c->d_tile_epoch) (void)hipFree(c->d_tile_epoch);
   if (c->d_counts) (void)hipFree(c->d_counts);
+  if (c->d_keys) (void)hipFree(c->d_keys);
+  if (c->d_hist) (void)hipFree(c->d_hist);
+  if (c->d_prio) (void)hipFree(c->d_prio);
+  if (c->d_trace) (void)hipFree(c->d_trace);
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->d_F) (void)hipFree(c->d_F);
   if (c->d_T) (void)hipFree(c->d_T);

@@ -37,7 +37,25 @@ struct PassArgs {
   uint32_t* count_clear;
   uint32_t* tile_epoch;
   unsigned long long* stats;  // kShards x kStatSlots
+  // ---- v4 (priority passes) only ----
+  unsigned long long* key_in;   // per-tile key of list p (double bits), reset to +inf by its reader
+  unsigned long long* key_out;  // keys of list p+1 (atomicMin)
+  const uint32_t* hist_in;      // kShards x kBins key histogram of list p
+  uint32_t* hist_out;           // ... of list p+1
+  uint32_t* hist_clear;         // ... of list p+2 (zeroed by block 0)
+  const unsigned long long* minkey_in;  // min key of list p
+  unsigned long long* minkey_out;
+  unsigned long long* minkey_clear;
+  const double* base_in;  // histogram origin of list p
+  double* base_out;       // ... of list p+1 (= min key of list p, written by block 0)
+  const double* delta;    // histogram bin width (k_prio_init)
+  uint32_t target;        // tiles to relax per pass; 0 = all (plain FIM)
+  float target_frac;      // ... at least this fraction of the active list
+  unsigned long long* trace;  // debug: kTracePts s_memrealtime stamps per block, or null
 };
+
+constexpr int kBins = 64;
+constexpr int kTracePts = 10;  // v4 key histogram bins
 
 hipError_t launch_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, int64_t row_hi,
                            hipStream_t st);
@@ -48,15 +66,25 @@ hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);        // v1: 32x32 tile / workgroup
 hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);     // v2: 8x8 tile / wave
+hipError_t launch_pass_prio(const PassArgs& a, int blocks, hipStream_t st,
+                           hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_pass_rb(const PassArgs& a, int blocks, hipStream_t st,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);     // v3: 2 x 8x8 tiles / wave, red-black
 hipError_t launch_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,
                                const double* new_lo, const double* new_hi, int ntx, int nty,
                                int tile_w, uint32_t* list, uint32_t* counts, uint32_t cap,
-                               uint32_t* tile_epoch, uint32_t epoch, hipStream_t st);
+                               uint32_t* tile_epoch, uint32_t epoch, unsigned long long* keys,
+                               uint32_t* hist, unsigned long long* minkey, const double* base,
+                               const double* delta, hipStream_t st);
 hipError_t launch_eikonal_batch(const double* tx, const double* ty, const double* c, double* out,
                                 uint64_t n, int fast, hipStream_t st);
 hipError_t launch_sum_counts(const uint32_t* counts, int32_t* out, hipStream_t st);
+hipError_t launch_prio_init(const double* F, int64_t ld, int64_t nx, int64_t ny,
+                           unsigned long long* keys, uint64_t nkeys, uint32_t* hist, uint64_t nhist,
+                           unsigned long long* minkey, double* base, double* delta, double kappa,
+                           hipStream_t st);
+hipError_t launch_prio_seed(unsigned long long* key0, uint32_t* hist0, unsigned long long* minkey0,
+                           uint32_t tile, double keyv, hipStream_t st);
 hipError_t launch_synth(double* F, uint64_t ld, uint32_t nx, uint32_t ny, uint64_t row0,
                         uint64_t seed, double frac, uint64_t oseed, int64_t gi, int64_t gj,
                         hipStream_t st);

@@ -690,6 +690,354 @@ __global__ __launch_bounds__(256) void k_fim_pass_rb(PassArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// v4 pass kernel: priority passes.  Plain FIM relaxes every
+// active tile every pass, so on rough fronts (random media) tiles far ahead of
+// the true front are relaxed many times with values that later improve again
+// (34 visits/tile at 16384^2).  Here every active tile carries a key -- a lower
+// bound on the values it can still take (the minimum changed edge value that
+// activated it) -- and a per-list key histogram (kBins bins of width delta from
+// the list's minimum key) gives every pass a threshold bin b*: only the ~target
+// lowest-key tiles are relaxed, the rest are re-appended unchanged (deferred,
+// never dropped, so the fixed point and the result are those of v3).
+// Keys are T values (>= 0 or +inf), ordered as u64 bit patterns.
+// ---------------------------------------------------------------------------
+constexpr unsigned long long kInfBits = 0x7FF0000000000000ull;
+constexpr int WCAP = 1024;  // LDS worklist of one classify chunk
+
+__device__ __forceinline__ unsigned long long dbits(double v) {
+  return (unsigned long long)__double_as_longlong(v);
+}
+__device__ __forceinline__ double bitsd(unsigned long long b) {
+  return __longlong_as_double((long long)b);
+}
+// Log-spaced bins: 4 per octave of (key - origin) / delta, so 64 bins span
+// delta * 2^16 -- fronts hundreds of cells deep -- with ~19% relative
+// resolution and no per-list rescaling.  Classification and histogram use this
+// same function, so a tile's bin is consistent between the two.
+__device__ __forceinline__ int key_bin(double k, double origin, double inv_delta) {
+  const float x = (float)((k - origin) * inv_delta);
+  if (!(x > 0.0f)) return 0;
+  const float b = 4.0f * __builtin_amdgcn_logf(1.0f + x);  // v_log_f32 (log2)
+  return b < (float)(kBins - 1) ? (int)b : kBins - 1;
+}
+
+__global__ __launch_bounds__(256) void k_fim_pass_prio(PassArgs a) {
+  __shared__ uint32_t s_q[QCAP];
+  __shared__ uint32_t s_work[WCAP];
+  __shared__ unsigned long long s_wkey[WCAP];
+  __shared__ uint32_t s_pref[kShards + 1];
+  __shared__ uint32_t s_hout[kBins];
+  __shared__ uint32_t s_nq, s_base, s_nwork;
+  __shared__ int s_bstar;
+  __shared__ unsigned long long s_visits, s_sweeps, s_minout;
+  __shared__ unsigned long long s_ek[8][4];
+  __shared__ double s_img[8][(WT + 2) * IP];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int half = lane >> 5;
+  const int hl = lane & 31;
+  const int r = hl >> 2, q = hl & 3;
+  const int cr = 2 * q + (r & 1), cb = 2 * q + 1 - (r & 1);
+  const uint32_t shard = blockIdx.x % kShards;
+  unsigned long long* trace = a.trace ? a.trace + (uint64_t)blockIdx.x * kTracePts : nullptr;
+  if (trace && tid == 0) trace[0] = __builtin_amdgcn_s_memrealtime();
+
+  // scalars first (independent loads, issued before the wave-0 scan)
+  const double delta = *a.delta;
+  const double origin_in = *a.base_in;            // bins of list p
+  const double origin_out = bitsd(*a.minkey_in);  // bins of list p+1
+  const double inv_delta = 1.0 / delta;
+  if (wv == 0) {
+    // list-shard prefix counts and the threshold bin, one wave, no serial loops
+    uint32_t c = lane < kShards ? a.count_in[lane] : 0u;
+    uint32_t h = 0;
+#pragma unroll
+    for (int k = 0; k < kShards; ++k) h += a.hist_in[k * kBins + lane];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t yc = __shfl_up(c, o), yh = __shfl_up(h, o);
+      if (lane >= o) {
+        c += yc;
+        h += yh;
+      }
+    }
+    if (lane < kShards) s_pref[lane + 1] = c;
+    const uint32_t n = __shfl(c, kShards - 1);
+    const uint32_t fr = (uint32_t)(a.target_frac * (float)n);
+    const uint32_t target = a.target > fr ? a.target : fr;
+    const unsigned long long m = __ballot(h >= target && lane < kBins - 1);
+    if (lane == 0) {
+      s_pref[0] = 0u;
+      s_bstar = (a.target > 0 && n > target && m) ? (int)__ffsll((long long)m) - 1 : kBins;
+      s_nq = 0;
+      s_visits = 0;
+      s_sweeps = 0;
+      s_minout = kInfBits;
+    }
+  }
+  s_hout[tid & (kBins - 1)] = 0u;
+  __syncthreads();
+  const uint32_t n_active = s_pref[kShards];
+  const int bstar = s_bstar;
+  if (trace && tid == 0) trace[1] = __builtin_amdgcn_s_memrealtime();
+  if (blockIdx.x == 0) {
+    if (tid < kShards) a.count_clear[tid] = 0u;
+    for (int k = tid; k < kShards * kBins; k += blockDim.x) a.hist_clear[k] = 0u;
+    if (tid == 0) {
+      *a.minkey_clear = kInfBits;
+      *a.base_out = origin_out;
+      if (n_active > 0) {
+        atomicAdd(&a.stats[kStatPasses], 1ull);
+        atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
+      }
+    }
+  }
+
+  // append tile t with key kb to list p+1 (key = running min over its activations)
+  auto enqueue = [&](uint32_t t, unsigned long long kb) {
+    atomicMin(&a.key_out[t], kb);
+    atomicMin(&s_minout, kb);
+    if (atomicMax(&a.tile_epoch[t], a.epoch) < a.epoch) {
+      atomicAdd(&s_hout[key_bin(bitsd(kb), origin_out, inv_delta)], 1u);
+      const uint32_t pos = atomicAdd(&s_nq, 1u);
+      if (pos < QCAP) {
+        s_q[pos] = t;
+      } else {
+        const uint32_t gp = atomicAdd(&a.count_out[shard], 1u);
+        a.list_out[(uint64_t)shard * a.shard_cap + gp] = t;
+      }
+    }
+  };
+
+  unsigned long long my_visits = 0, my_sweeps = 0;
+  double* img = s_img[wv * 2 + half];
+  unsigned long long* ek = s_ek[wv * 2 + half];
+  const int sr = (r + 1) * IP + (cr + 1);
+  const int sb = (r + 1) * IP + (cb + 1);
+  const unsigned long long hmask = half ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+
+  const uint32_t chunk = (n_active + gridDim.x - 1) / gridDim.x;
+  const uint32_t c0 = blockIdx.x * chunk;
+  const uint32_t c1 = min(n_active, c0 + chunk);
+  for (uint32_t s0 = c0; s0 < c1; s0 += WCAP) {  // block-uniform
+    const uint32_t s1 = min(c1, s0 + WCAP);
+    if (tid == 0) s_nwork = 0;
+    __syncthreads();
+    for (uint32_t e = s0 + tid; e < s1; e += blockDim.x) {
+      const uint32_t t = list_at(a.list_in, a.shard_cap, s_pref, e);
+      const unsigned long long kb = a.key_in[t];
+      a.key_in[t] = kInfBits;
+      if (key_bin(bitsd(kb), origin_in, inv_delta) <= bstar) {
+        const uint32_t pos = atomicAdd(&s_nwork, 1u);
+        s_work[pos] = t;
+        s_wkey[pos] = kb;
+      } else {
+        enqueue(t, kb);  // deferred
+      }
+    }
+    __syncthreads();
+    const uint32_t nw = s_nwork;
+    if (trace && tid == 0 && s0 == c0) trace[2] = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t wb = (uint32_t)wv * 2u; wb < nw; wb += 8u) {  // wave-uniform
+      const uint32_t li = wb + (uint32_t)half;
+      const bool has = li < nw;
+      uint32_t tile = 0;
+      int tx = 0, ty = 0;
+      if (has) {
+        tile = s_work[li];
+        tx = (int)(tile % (uint32_t)a.ntx);
+        ty = (int)(tile / (uint32_t)a.ntx);
+      }
+      if (hl < 4) ek[hl] = kInfBits;
+      const int64_t i0 = (int64_t)tx * WT, j0 = (int64_t)ty * WT;
+      const int64_t gj = j0 + r, gir = i0 + cr, gib = i0 + cb;
+      const bool rowin = has && gj < a.ny;
+      double tr = dinf(), fr = dinf(), tb = dinf(), fb = dinf();
+      if (rowin && gir < a.nx) {
+        tr = a.T[gj * a.ld + gir];
+        fr = a.F[gj * a.ld + gir];
+      }
+      if (rowin && gib < a.nx) {
+        tb = a.T[gj * a.ld + gib];
+        fb = a.F[gj * a.ld + gib];
+      }
+      double hw = dinf(), he = dinf(), hs0 = dinf(), hs1 = dinf(), hn0 = dinf(), hn1 = dinf();
+      if (rowin) {
+        if (q == 0 && i0 > 0) hw = a.T[gj * a.ld + (i0 - 1)];
+        if (q == 3 && i0 + WT < a.nx) he = a.T[gj * a.ld + (i0 + WT)];
+      }
+      if (has) {
+        const int64_t cc0 = i0 + 2 * q, cc1 = cc0 + 1;
+        if (r == 0 && (j0 > 0 || a.ghost_lo)) {
+          if (cc0 < a.nx) hs0 = a.T[(j0 - 1) * a.ld + cc0];
+          if (cc1 < a.nx) hs1 = a.T[(j0 - 1) * a.ld + cc1];
+        }
+        if (r == WT - 1) {
+          const int64_t jn = j0 + WT;
+          if (jn < a.ny || (jn == a.ny && a.ghost_hi)) {
+            if (cc0 < a.nx) hn0 = a.T[jn * a.ld + cc0];
+            if (cc1 < a.nx) hn1 = a.T[jn * a.ld + cc1];
+          }
+        }
+      }
+      {
+        const int row = (r + 1) * IP;
+        if (q == 0) img[row] = hw;
+        if (q == 3) img[row + WT + 1] = he;
+        if (r == 0) {
+          img[1 + 2 * q] = hs0;
+          img[2 + 2 * q] = hs1;
+        }
+        if (r == WT - 1) {
+          img[(WT + 1) * IP + 1 + 2 * q] = hn0;
+          img[(WT + 1) * IP + 2 + 2 * q] = hn1;
+        }
+        img[sb] = tb;
+      }
+      const double tr0 = tr, tb0 = tb;
+      if (trace && tid == 0 && wb == 0) {
+        __builtin_amdgcn_s_waitcnt(0);
+        trace[6] = __builtin_amdgcn_s_memrealtime();
+      }
+      const bool fast = __all(!(fr < kFastMinF) && !(fb < kFastMinF));
+      bool capped;
+      const int sweeps = fast ? rb_sweeps<true>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped)
+                              : rb_sweeps<false>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped);
+      if (has) {
+        my_visits += 1;
+        my_sweeps += (unsigned long long)sweeps;
+      }
+      if (trace && tid == 0 && wb == 0) trace[7] = __builtin_amdgcn_s_memrealtime();
+      const bool dr = tr < tr0, db = tb < tb0;
+      if (dr) a.T[gj * a.ld + gir] = tr;
+      if (db) a.T[gj * a.ld + gib] = tb;
+      // minimum decreased value on each edge: the key of the neighbour it wakes
+      {
+        const unsigned long long vr = dr ? dbits(tr) : kInfBits;
+        const unsigned long long vb = db ? dbits(tb) : kInfBits;
+        const unsigned long long vrb = vr < vb ? vr : vb;
+        if (r == 0 && vrb != kInfBits) atomicMin(&ek[0], vrb);
+        if (r == WT - 1 && vrb != kInfBits) atomicMin(&ek[3], vrb);
+        const unsigned long long vw = cr == 0 ? vr : (cb == 0 ? vb : kInfBits);
+        const unsigned long long ve = cr == WT - 1 ? vr : (cb == WT - 1 ? vb : kInfBits);
+        if (vw != kInfBits) atomicMin(&ek[1], vw);
+        if (ve != kInfBits) atomicMin(&ek[2], ve);
+      }
+      const unsigned long long mC = __ballot(capped && has) & hmask;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      bool want = false;
+      int nx_t = tx, ny_t = ty;
+      unsigned long long kb = kInfBits;
+      if (has && hl < 4) {
+        kb = ek[hl];
+        if (hl == 0) { want = kb != kInfBits && ty > 0; ny_t = ty - 1; }
+        else if (hl == 1) { want = kb != kInfBits && tx > 0; nx_t = tx - 1; }
+        else if (hl == 2) { want = kb != kInfBits && tx + 1 < a.ntx; nx_t = tx + 1; }
+        else { want = kb != kInfBits && ty + 1 < a.nty; ny_t = ty + 1; }
+      } else if (has && hl == 4 && mC != 0ull) {
+        want = true;
+        kb = s_wkey[li];
+      }
+      if (want) enqueue((uint32_t)ny_t * (uint32_t)a.ntx + (uint32_t)nx_t, kb);
+      __builtin_amdgcn_wave_barrier();
+      if (trace && wb == 0) {
+        __builtin_amdgcn_s_waitcnt(0);
+        if (tid == 0) trace[8] = __builtin_amdgcn_s_memrealtime();
+      }
+    }
+    __syncthreads();
+  }
+  if (trace && tid == 0) trace[3] = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && my_visits) {
+    atomicAdd(&s_visits, my_visits);
+    atomicAdd(&s_sweeps, my_sweeps);
+  }
+  if (lane == 32 && my_visits) {
+    atomicAdd(&s_visits, my_visits);
+    atomicAdd(&s_sweeps, my_sweeps);
+  }
+  __syncthreads();
+  const uint32_t nq = s_nq < QCAP ? s_nq : QCAP;
+  if (tid == 0) {
+    if (nq) s_base = atomicAdd(&a.count_out[shard], nq);
+    if (s_minout != kInfBits) atomicMin(a.minkey_out, s_minout);
+    if (s_visits) {
+      unsigned long long* st = a.stats + (uint64_t)shard * kStatSlots;
+      atomicAdd(&st[kStatVisits], s_visits);
+      atomicAdd(&st[kStatSweeps], s_sweeps);
+    }
+  }
+  if (tid < kBins && s_hout[tid]) atomicAdd(&a.hist_out[shard * kBins + tid], s_hout[tid]);
+  __syncthreads();
+  for (uint32_t k = tid; k < nq; k += blockDim.x)
+    a.list_out[(uint64_t)shard * a.shard_cap + s_base + k] = s_q[k];
+  if (trace && tid == 0) {
+    trace[4] = __builtin_amdgcn_s_memrealtime();
+    trace[5] = ((unsigned long long)(c1 > c0 ? c1 - c0 : 0) << 32) | (unsigned long long)s_visits;
+  }
+}
+
+// Priority-pass state for a new solve: every key +inf, histograms zero, list-0
+// origin 0, bin width delta = kappa * mean finite F over a strided sample.
+__global__ void k_prio_init(const double* F, int64_t ld, int64_t nx, int64_t ny,
+                            unsigned long long* keys, uint64_t nkeys, uint32_t* hist,
+                            uint64_t nhist, unsigned long long* minkey, double* base,
+                            double* delta, double kappa) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nkeys;
+       k += (uint64_t)gridDim.x * blockDim.x)
+    keys[k] = kInfBits;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nhist;
+       k += (uint64_t)gridDim.x * blockDim.x)
+    hist[k] = 0u;
+  if (blockIdx.x == 0) {
+    __shared__ double s_sum[256];
+    __shared__ uint32_t s_cnt[256];
+    const int64_t ncell = nx * ny;
+    const int64_t ns = ncell < 65536 ? ncell : 65536;
+    double sum = 0.0;
+    uint32_t cnt = 0;
+    for (int64_t k = threadIdx.x; k < ns; k += blockDim.x) {
+      const int64_t c = (k * ncell) / ns;  // strided sample
+      const double f = F[(c / nx) * ld + (c % nx)];
+      if (f < dinf()) {
+        sum += f;
+        ++cnt;
+      }
+    }
+    s_sum[threadIdx.x] = sum;
+    s_cnt[threadIdx.x] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = 0.0;
+      uint32_t c = 0;
+      for (int k = 0; k < (int)blockDim.x; ++k) {
+        s += s_sum[k];
+        c += s_cnt[k];
+      }
+      const double mean = c ? s / (double)c : 1.0;
+      *delta = (mean > 0.0 && mean < dinf()) ? kappa * mean : 1.0;
+      for (int k = 0; k < 3; ++k) {
+        minkey[k] = kInfBits;
+        base[k] = 0.0;
+      }
+    }
+  }
+}
+
+// The goal tile (or a re-seeded tile) enters list 0 with key keyv, bin 0.
+__global__ void k_prio_seed(unsigned long long* key0, uint32_t* hist0, unsigned long long* minkey0,
+                            uint32_t tile, double keyv) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    key0[tile] = dbits(keyv);
+    hist0[0] += 1u;
+    *minkey0 = dbits(keyv);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Sharded (row-slab) mode: merge freshly received neighbour rows into the
 // ghost rows (values only decrease, so a min-merge) and seed the tiles of the
 // first / last tile row under every column that improved, into the list the
@@ -698,7 +1046,9 @@ __global__ __launch_bounds__(256) void k_fim_pass_rb(PassArgs a) {
 __global__ void k_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,
                                const double* new_lo, const double* new_hi, int ntx, int nty,
                                int tile_w, uint32_t* list, uint32_t* counts, uint32_t cap,
-                               uint32_t* tile_epoch, uint32_t epoch) {
+                               uint32_t* tile_epoch, uint32_t epoch, unsigned long long* keys,
+                               uint32_t* hist, unsigned long long* minkey, const double* base,
+                               const double* delta) {
   // blocks of 256 threads start at multiples of 256 columns and tile_w divides
   // 64, so a tile's columns are tile_w consecutive lanes of one wave.
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -709,20 +1059,31 @@ __global__ void k_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,
     const double* src = side == 0 ? new_lo : new_hi;
     if (!src) continue;  // uniform
     bool seed = false;
+    double v = dinf();
     if (k < nx) {
       double* g = T + (side == 0 ? -ld : nrows * ld) + k;
-      const double v = src[k];
+      v = src[k];
       if (v < *g) {
         *g = v;
         seed = true;
       }
     }
     const unsigned long long m = __ballot(seed);
+    const uint32_t tile = (uint32_t)((side == 0 ? 0 : nty - 1) * (int64_t)ntx + k / tile_w);
+    if (keys) {  // v4: key = min improved ghost value under the tile
+      if (seed) atomicMin(&keys[tile], dbits(v));
+      double wm = seed ? v : dinf();
+      for (int o = 32; o > 0; o >>= 1) wm = vmin64(wm, __shfl_xor(wm, o));
+      if (lane == 0 && wm < dinf()) atomicMin(minkey, dbits(wm));
+    }
     if (k < nx && (k % tile_w) == 0 && ((m >> lane) & tmask)) {
-      const uint32_t tile = (uint32_t)((side == 0 ? 0 : nty - 1) * (int64_t)ntx + k / tile_w);
       if (atomicMax(&tile_epoch[tile], epoch) < epoch) {
         const uint32_t pos = atomicAdd(&counts[shard], 1u);
         list[(uint64_t)shard * cap + pos] = tile;
+        if (keys) {
+          const double kv = bitsd(keys[tile]);
+          atomicAdd(&hist[shard * kBins + key_bin(kv, *base, 1.0 / *delta)], 1u);
+        }
       }
     }
   }
@@ -804,6 +1165,33 @@ hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st, hipEven
   return hipGetLastError();
 }
 
+hipError_t launch_pass_prio(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
+                            hipEvent_t e1) {
+  if (e0 || e1)
+    hipExtLaunchKernelGGL(k_fim_pass_prio, dim3(blocks), dim3(256), 0, st, e0, e1, 0, a);
+  else
+    hipLaunchKernelGGL(k_fim_pass_prio, dim3(blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_prio_init(const double* F, int64_t ld, int64_t nx, int64_t ny,
+                            unsigned long long* keys, uint64_t nkeys, uint32_t* hist,
+                            uint64_t nhist, unsigned long long* minkey, double* base,
+                            double* delta, double kappa, hipStream_t st) {
+  uint64_t nb = (nkeys + 255) / 256;
+  if (nb > 4096) nb = 4096;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(k_prio_init, dim3((unsigned)nb), dim3(256), 0, st, F, ld, nx, ny, keys, nkeys,
+                     hist, nhist, minkey, base, delta, kappa);
+  return hipGetLastError();
+}
+
+hipError_t launch_prio_seed(unsigned long long* key0, uint32_t* hist0, unsigned long long* minkey0,
+                            uint32_t tile, double keyv, hipStream_t st) {
+  hipLaunchKernelGGL(k_prio_seed, dim3(1), dim3(64), 0, st, key0, hist0, minkey0, tile, keyv);
+  return hipGetLastError();
+}
+
 hipError_t launch_pass_rb(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
   if (e0 || e1)  // timestamps taken by the dispatch itself (no extra stream packets)
     hipExtLaunchKernelGGL(k_fim_pass_rb, dim3(blocks), dim3(256), 0, st, e0, e1, 0, a);
@@ -829,11 +1217,14 @@ hipError_t launch_eikonal_batch(const double* tx, const double* ty, const double
 hipError_t launch_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,
                                const double* new_lo, const double* new_hi, int ntx, int nty,
                                int tile_w, uint32_t* list, uint32_t* counts, uint32_t cap,
-                               uint32_t* tile_epoch, uint32_t epoch, hipStream_t st) {
+                               uint32_t* tile_epoch, uint32_t epoch, unsigned long long* keys,
+                               uint32_t* hist, unsigned long long* minkey, const double* base,
+                               const double* delta, hipStream_t st) {
   const unsigned blocks = (unsigned)((nx + 255) / 256);
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(k_merge_ghosts, dim3(blocks), dim3(256), 0, st, T, ld, nx, nrows, new_lo,
-                     new_hi, ntx, nty, tile_w, list, counts, cap, tile_epoch, epoch);
+                     new_hi, ntx, nty, tile_w, list, counts, cap, tile_epoch, epoch, keys, hist,
+                     minkey, base, delta);
   return hipGetLastError();
 }
 

@@ -46,6 +46,8 @@ class DymuOpts(ctypes.Structure):
         ("max_passes", ctypes.c_int),
         ("max_inner", ctypes.c_int),
         ("grid_blocks", ctypes.c_int),
+        ("kernel", ctypes.c_int),
+        ("prio_target", ctypes.c_int),
     ]
 
 
@@ -72,6 +74,8 @@ class DymuStats(ctypes.Structure):
         ("ms", ctypes.c_double),
         ("tile_w", ctypes.c_int),
         ("tile_h", ctypes.c_int),
+        ("kernel", ctypes.c_int),
+        ("reserved", ctypes.c_int),
     ]
 
     def as_dict(self) -> dict:
@@ -152,10 +156,12 @@ class Engine:
     """One HIP context (stream + workspace) on one device."""
 
     def __init__(self, device: int = -1, passes_per_check: int = 0, max_passes: int = 0,
-                 max_inner: int = 0, grid_blocks: int = 0):
+                 max_inner: int = 0, grid_blocks: int = 0, kernel: int = 0,
+                 prio_target: int = 0):
         lib = load_fim()
         self._lib = lib
-        opts = DymuOpts(device, passes_per_check, max_passes, max_inner, grid_blocks)
+        opts = DymuOpts(device, passes_per_check, max_passes, max_inner, grid_blocks, kernel,
+                        prio_target)
         ctx = _vp()
         rc = lib.dymu_create(ctypes.byref(ctx), ctypes.byref(opts))
         if rc != DYMU_OK:

@@ -48,3 +48,15 @@ def engine(dymu):
     eng = dymu.Engine()
     yield eng
     eng.close()
+
+
+# pass kernels under test: 3 = plain block FIM, 4 = priority passes with a small
+# per-pass target so that deferral happens even on test-sized grids
+KERNELS = {"fim": dict(kernel=3), "prio": dict(kernel=4, prio_target=64)}
+
+
+@pytest.fixture(scope="session", params=sorted(KERNELS))
+def kengine(request, dymu):
+    eng = dymu.Engine(**KERNELS[request.param])
+    yield eng
+    eng.close()

@@ -37,7 +37,7 @@ def test_planner_exports_every_declared_symbol(dymu):
 
 def test_abi_version_and_strerror(dymu):
     lib = dymu.load_fim()
-    assert lib.dymu_abi_version() == 1
+    assert lib.dymu_abi_version() == 2
     assert lib.dymu_strerror(-4) == b"pass cap reached before convergence"
 
 

@@ -19,7 +19,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, nx, ny, goal, F_full, out_q):
+def _worker(rank, world, port, nx, ny, goal, F_full, out_q, engine_kw):
     import sys
     import torch  # first: one HIP runtime for torch and libdymu_fim
     import torch.distributed as dist
@@ -34,7 +34,7 @@ def _worker(rank, world, port, nx, ny, goal, F_full, out_q):
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
         row0, nrows = dymu.slab_rows(ny, world, rank)
-        eng = dymu.Engine(device=0)
+        eng = dymu.Engine(device=0, **engine_kw)
         F = torch.from_numpy(np.ascontiguousarray(F_full[row0:row0 + nrows])).to(dev)
         T_buf = torch.empty((nrows + 2, nx), dtype=torch.float64, device=dev)
         solver = SlabSolver(eng, nx, ny, rank, world, row0, nrows, dev,
@@ -49,14 +49,16 @@ def _worker(rank, world, port, nx, ny, goal, F_full, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,nx,ny,goal", [(2, 300, 256, (150, 128)), (3, 200, 230, (20, 30))])
-def test_gpu_sharded_matches_oracle(oracle, world, nx, ny, goal):
+@pytest.mark.parametrize("world,nx,ny,goal,engine_kw", [
+    (2, 300, 256, (150, 128), dict(kernel=3)),
+    (3, 200, 230, (20, 30), dict(kernel=4, prio_target=32))])
+def test_gpu_sharded_matches_oracle(oracle, world, nx, ny, goal, engine_kw):
     import torch.multiprocessing as mp
     F = oracle.synth_speed(nx, ny, seed=41, obst_frac=0.03, obst_seed=43, goal=goal)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, nx, ny, goal, F, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, nx, ny, goal, F, q, engine_kw))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -8,12 +8,12 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def solve_virtual_slabs(dymu, F, goal, S, K=8):
+def solve_virtual_slabs(dymu, F, goal, S, K=8, **engine_kw):
     ny, nx = F.shape
     slabs = []
     for s in range(S):
         row0, nrows = dymu.slab_rows(ny, S, s)
-        eng = dymu.Engine()
+        eng = dymu.Engine(**engine_kw)
         dF = eng.alloc(8 * nrows * nx)
         dT = eng.alloc(8 * (nrows + 2) * nx)
         stage = eng.alloc(16 * nx)
@@ -60,9 +60,11 @@ def solve_virtual_slabs(dymu, F, goal, S, K=8):
 @pytest.mark.parametrize("S,nx,ny,goal,frac", [(2, 200, 160, (100, 40), 0.02),
                                                (3, 130, 200, (7, 190), 0.05),
                                                (4, 256, 256, (128, 128), 0.0)])
-def test_virtual_slabs_match_oracle(dymu, oracle, S, nx, ny, goal, frac):
+@pytest.mark.parametrize("kw", [dict(kernel=3), dict(kernel=4, prio_target=32)],
+                         ids=["fim", "prio"])
+def test_virtual_slabs_match_oracle(dymu, oracle, S, nx, ny, goal, frac, kw):
     F = oracle.synth_speed(nx, ny, seed=31, obst_frac=frac, obst_seed=5, goal=goal)
-    T, rounds = solve_virtual_slabs(dymu, F, goal, S)
+    T, rounds = solve_virtual_slabs(dymu, F, goal, S, **kw)
     Tref, _ = oracle.fmm(F, goal)
     assert np.array_equal(np.isinf(T), np.isinf(Tref))
     fin = np.isfinite(Tref)

@@ -21,12 +21,12 @@ def assert_parity(T, Tref):
     return err.max(initial=0.0)
 
 
-def test_kat_mt19937_256(engine, oracle):
+def test_kat_mt19937_256(kengine, oracle):
     """SURVEY s8(c) KAT: reference sum(getTotalCostMatrix)=1.7066083890e+07,
     T[1][1]=479.2433625750 at N=256."""
     N = 256
     F = oracle.mt_uniform(N * N).reshape(N, N)
-    r = engine.solve(F, N // 2, N // 2)
+    r = kengine.solve(F, N // 2, N // 2)
     M = np.where(np.isinf(r.T), -1.0, r.T)
     assert f"{M.sum():.10e}" == "1.7066083890e+07"
     assert f"{r.T[1, 1]:.10f}" == "479.2433625750"
@@ -35,11 +35,11 @@ def test_kat_mt19937_256(engine, oracle):
 
 
 @pytest.mark.parametrize("N", [512, 1024])
-def test_kat_mt19937(engine, oracle, N):
+def test_kat_mt19937(kengine, oracle, N):
     kat = {512: ("1.3467278246e+08", "972.7322452271"),
            1024: ("1.0666255888e+09", "1913.6136177798")}[N]
     F = oracle.mt_uniform(N * N).reshape(N, N)
-    r = engine.solve(F, N // 2, N // 2)
+    r = kengine.solve(F, N // 2, N // 2)
     M = np.where(np.isinf(r.T), -1.0, r.T)
     assert f"{M.sum():.10e}" == kat[0]
     assert f"{r.T[1, 1]:.10f}" == kat[1]
@@ -55,9 +55,9 @@ def test_kat_mt19937(engine, oracle, N):
     (257, 129, 0.10, (128, 64)),
     (500, 700, 0.25, (250, 350)),    # dense obstacles, disconnected pockets
 ])
-def test_parity_random(engine, oracle, nx, ny, frac, goal):
+def test_parity_random(kengine, oracle, nx, ny, frac, goal):
     F = oracle.synth_speed(nx, ny, seed=7, obst_frac=frac, obst_seed=11, goal=goal)
-    r = engine.solve(F, goal[0], goal[1])
+    r = kengine.solve(F, goal[0], goal[1])
     Tref, _ = oracle.fmm(F, goal)
     assert_parity(r.T, Tref)
     assert r.T[goal[1], goal[0]] == 0.0
@@ -99,13 +99,47 @@ def test_device_resident_and_synth(engine, oracle):
         engine.free(dT)
 
 
-def test_repeat_solves_reuse_context(engine, oracle):
-    """Epoch-stamped tile flags survive across solves of different sizes."""
-    for (nx, ny, g) in [(200, 200, (100, 100)), (64, 300, (3, 5)), (200, 200, (20, 180))]:
+def test_repeat_solves_reuse_context(kengine, oracle):
+    """Epoch-stamped tile flags and priority keys survive across solves of
+    different sizes."""
+    for (nx, ny, g) in [(200, 200, (100, 100)), (64, 300, (3, 5)), (200, 200, (20, 180)),
+                        (700, 500, (10, 490))]:
         F = oracle.synth_speed(nx, ny, seed=5, obst_frac=0.03, obst_seed=9, goal=g)
-        r = engine.solve(F, g[0], g[1])
+        r = kengine.solve(F, g[0], g[1])
         Tref, _ = oracle.fmm(F, g)
         assert_parity(r.T, Tref)
+
+
+def test_priority_kernel_defers(dymu, oracle):
+    """Kernel 4 with a small target relaxes fewer tiles than plain FIM and
+    reaches the same map; the stats report which kernel ran."""
+    nx = ny = 1024
+    g = (512, 512)
+    F = oracle.synth_speed(nx, ny, seed=2, obst_frac=0.02, obst_seed=4, goal=g)
+    out = {}
+    for k, kw in ((3, {}), (4, dict(prio_target=256))):
+        eng = dymu.Engine(kernel=k, **kw)
+        try:
+            out[k] = eng.solve(F, g[0], g[1])
+        finally:
+            eng.close()
+    assert out[3].stats["kernel"] == 3 and out[4].stats["kernel"] == 4
+    assert out[4].stats["tile_visits"] < out[3].stats["tile_visits"]
+    Tref, _ = oracle.fmm(F, g)
+    assert_parity(out[3].T, Tref)
+    assert_parity(out[4].T, Tref)
+
+
+def test_auto_kernel_choice(dymu):
+    """kernel=0 picks plain FIM below 2^19 8x8 tiles (~5800^2 cells)."""
+    eng = dymu.Engine()
+    try:
+        r = eng.solve(np.ones((64, 64)), 3, 3)
+        assert r.stats["kernel"] == 3
+    finally:
+        eng.close()
+    with pytest.raises(dymu.DymuError):
+        dymu.Engine(kernel=7)
 
 
 def test_bad_args(engine, dymu):

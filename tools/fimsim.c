@@ -225,6 +225,11 @@ static int solve_tile(int tx, int ty, int method, int maxs, int* sweeps_out, uns
   return s >= maxs;
 }
 
+int cmpd(const void* a, const void* b) {
+  double x = *(const double*)a, y = *(const double*)b;
+  return x < y ? -1 : x > y;
+}
+
 int main(int argc, char** argv) {
   INF = __builtin_inf();
   N = atoi(argv[1]);
@@ -272,6 +277,18 @@ int main(int argc, char** argv) {
     double kmin = INF;
     for (int q = 0; q < nc; q++) if (key[cur[q]] < kmin) kmin = key[cur[q]];
     double thr = DELTA > 0 ? kmin + DELTA : INF;
+    if (getenv("TARGET")) {  // relax the TARGET lowest keys (v4 model)
+      int P = atoi(getenv("TARGET"));
+      if (nc > P) {
+        static double* kk = 0;
+        static int kcap = 0;
+        if (kcap < nc) { kk = realloc(kk, sizeof(double) * nc); kcap = nc; }
+        for (int q = 0; q < nc; q++) kk[q] = key[cur[q]];
+        int cmpd(const void* a, const void* b);
+        qsort(kk, nc, sizeof(double), cmpd);
+        thr = kk[P - 1];
+      }
+    }
     for (int q = 0; q < nc; q++) {
       int t = cur[q], tx = t % ntx, ty = t / ntx, sw;
       if (key[t] > thr) {  // deferred: stays active
