@@ -149,12 +149,14 @@ int dymu_device_free(dymu_ctx* ctx, void* dptr);
 int dymu_memcpy_d2h(dymu_ctx* ctx, void* dst, const void* src, size_t bytes);
 int dymu_memcpy_h2d(dymu_ctx* ctx, void* dst, const void* src, size_t bytes);
 
-/* Profiling: when on, every pass launch is bracketed by HIP events so
- * dymu_last_pass_timing() reports pure kernel time (adds event overhead). */
-int dymu_set_profiling(dymu_ctx* ctx, int on);
+/* Profiling: period > 0 times every period-th pass launch with HIP events
+ * (start/stop taken by the dispatch itself); 0 turns it off.  Sampling keeps
+ * the event overhead out of the timed region (period 1 costs ~4 us/launch). */
+int dymu_set_profiling(dymu_ctx* ctx, int period);
 
-/* Kernel time of the most recent solve's pass launches (ms, HIP events on
- * the launch stream) and their count -- the bench's roofline source. */
+/* Summed kernel time (ms, HIP events on the launch stream) of the most recent
+ * solve's SAMPLED pass launches and their count: the mean launch duration is
+ * pass_ms_total / n_pass_launches -- the bench's roofline source. */
 int dymu_last_pass_timing(dymu_ctx* ctx, double* pass_ms_total, uint64_t* n_pass_launches);
 
 const char* dymu_strerror(int status);

@@ -83,6 +83,7 @@ struct dymu_ctx {
   std::vector<hipEvent_t> prof_ev;
   double last_pass_ms = 0.0;
   uint64_t last_launches = 0;
+  uint64_t last_timed = 0;  // sampled launches behind last_pass_ms
 
   std::string last_error;
 };
@@ -263,7 +264,7 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
       a.trace = c->d_trace;
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (prof) {
+    if (prof && D.launches % (uint64_t)c->profiling == 0) {
       while (c->prof_ev.size() < D.prof_used + 2) {
         hipEvent_t e;
         HIPC(c, hipEventCreate(&e));
@@ -357,7 +358,9 @@ int dom_finish(dymu_ctx* c, hipStream_t st, dymu_stats* stats, double ms) {
   c->epoch_base = D.eb + (uint32_t)D.p + 4u;
   c->last_launches = D.launches;
   c->last_pass_ms = 0.0;
+  c->last_timed = 0;
   if (c->profiling) {
+    c->last_timed = D.prof_used / 2;
     for (size_t q = 0; q + 1 < D.prof_used; q += 2) {
       float m = 0.f;
       HIPC(c, hipEventElapsedTime(&m, c->prof_ev[q], c->prof_ev[q + 1]));
@@ -647,16 +650,16 @@ int dymu_eikonal_batch(dymu_ctx* c, const double* tx, const double* ty, const do
   return DYMU_OK;
 }
 
-int dymu_set_profiling(dymu_ctx* c, int on) {
-  if (!c) return DYMU_ERR_ARG;
-  c->profiling = on;
+int dymu_set_profiling(dymu_ctx* c, int period) {
+  if (!c || period < 0) return DYMU_ERR_ARG;
+  c->profiling = period;
   return DYMU_OK;
 }
 
 int dymu_last_pass_timing(dymu_ctx* c, double* ms, uint64_t* n) {
   if (!c) return DYMU_ERR_ARG;
   if (ms) *ms = c->last_pass_ms;
-  if (n) *n = c->last_launches;
+  if (n) *n = c->last_timed;
   return DYMU_OK;
 }
 

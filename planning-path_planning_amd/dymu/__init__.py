@@ -270,8 +270,9 @@ class Engine:
             for p in ptrs:
                 self.free(p)
 
-    def set_profiling(self, on: bool):
-        _check(self._lib.dymu_set_profiling(self.ctx, 1 if on else 0), self.ctx)
+    def set_profiling(self, period):
+        """Time every `period`-th pass launch (True = every launch, 0/False = off)."""
+        _check(self._lib.dymu_set_profiling(self.ctx, int(period)), self.ctx)
 
     def last_pass_timing(self):
         ms, n = ctypes.c_double(), ctypes.c_uint64()

@@ -172,3 +172,23 @@ def test_update_arithmetic_bit_exact(engine, oracle, fast):
     with np.errstate(invalid="ignore"):
         r = np.where(two, (tx + ty + np.sqrt(2 * (c * c) - d * d)) / 2, np.minimum(tx, ty) + c)
     assert np.array_equal(out, r)
+
+
+def test_sampled_pass_timing(dymu, oracle):
+    """dymu_set_profiling(period) times every period-th pass launch."""
+    nx = ny = 512
+    F = oracle.synth_speed(nx, ny, seed=3, obst_frac=0.02, obst_seed=5, goal=(256, 256))
+    eng = dymu.Engine()
+    try:
+        eng.set_profiling(4)
+        r = eng.solve(F, 256, 256)
+        ms, n = eng.last_pass_timing()
+        L = r.stats["launches"]
+        assert n == (L + 3) // 4 and ms > 0.0
+        eng.set_profiling(0)
+        eng.solve(F, 256, 256)
+        assert eng.last_pass_timing() == (0.0, 0)
+        with pytest.raises(dymu.DymuError):
+            eng.set_profiling(-1)
+    finally:
+        eng.close()

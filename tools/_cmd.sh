@@ -1,5 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/gpu_tests.log; exit 1; }
-tail -3 gpurun_out/gpu_tests.log
-SIZES="8192" RUNS="DYMU_KERNEL=3;DYMU_KERNEL=4;DYMU_KERNEL=4 DYMU_PRIO_TARGET=8192" bash tools/sweep.sh
+timeout -k 10 300 python -m pytest tests/test_gpu_solver.py -x -q > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/gpu_tests.log
+timeout -k 10 300 python bench.py --cpu-sample 0 > gpurun_out/bench_a.log 2>&1 && timeout -k 10 300 python bench.py --cpu-sample 0 --no-profile > gpurun_out/bench_b.log 2>&1
