@@ -55,9 +55,11 @@ typedef struct dymu_opts {
   int max_passes;       /* safety cap on FIM passes; 0 = derived from the grid size */
   int max_inner;        /* cap on in-tile sweeps per tile visit; 0 = default */
   int grid_blocks;      /* workgroups per pass launch; 0 = derived from the device */
-  int kernel;           /* pass kernel: 0 = auto (by grid size), 3 = plain block FIM,
-                           4 = priority passes */
-  int prio_target;      /* kernel 4: tiles relaxed per pass; 0 = default (64 per CU) */
+  int kernel;           /* pass kernel: 0 = auto (by grid size), 3 = plain block FIM
+                           (8x8 tiles), 4 = priority passes on 8x8 tiles, 5 = priority
+                           passes on 16x16 tiles */
+  int prio_target;      /* kernels 4/5: tiles relaxed per pass; 0 = default
+                           (64 per CU for 4, 8 per CU for 5) */
 } dymu_opts;
 
 typedef struct dymu_stats {

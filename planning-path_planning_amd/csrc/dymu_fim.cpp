@@ -31,11 +31,12 @@ struct dymu_ctx {
 
   // 1: 32x32 tile per workgroup, 2: 8x8 tile per wave (Jacobi),
   // 3: two 8x8 tiles per wave (red-black), 4: v3 body + priority passes;
-  // 0 (default): per domain, 4 from prio_min_tiles 8x8 tiles up, else 3.
+  // 5: priority passes on 16x16 tiles (one per wave);
+  // 0 (default): per domain, 5 from prio_min_tiles 8x8 tiles up, else 3.
   // DYMU_KERNEL overrides
   int variant = 0;
-  uint32_t prio_min_tiles = 1u << 19;  // DYMU_PRIO_MIN_TILES
-  uint32_t prio_target = 0;  // v4: tiles relaxed per pass (DYMU_PRIO_TARGET)
+  uint32_t prio_min_tiles = 1u << 17;  // DYMU_PRIO_MIN_TILES (~2900^2 cells)
+  uint32_t prio_target = 0;  // v4/v5: tiles relaxed per pass; 0 = per-variant default
   double prio_kappa = 0.5;   // v4: histogram bin width / mean F (DYMU_PRIO_KAPPA)
   float prio_frac = 0.0f;    // v4: ... or this fraction of the active list (DYMU_PRIO_FRAC)
   int prio_trace = -1;       // v4: stamp phases of this pass index (DYMU_PRIO_TRACE)
@@ -152,8 +153,9 @@ unsigned long long* prio_keys(dymu_ctx* c, uint64_t q) {
   return c->d_keys + q * (uint64_t)c->dom.ntiles;
 }
 
-int tile_w(int variant) { return variant == 1 ? kTileW : kWaveTile; }
-int tile_h(int variant) { return variant == 1 ? kTileH : kWaveTile; }
+int tile_w(int variant) { return variant == 1 ? kTileW : variant == 5 ? 16 : kWaveTile; }
+int tile_h(int variant) { return variant == 1 ? kTileH : variant == 5 ? 16 : kWaveTile; }
+bool is_prio(int variant) { return variant == 4 || variant == 5; }
 
 // ---- domain primitives (whole grid, or one row slab with ghost rows) ----
 int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t nrows, uint64_t ld,
@@ -163,7 +165,7 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   if (variant == 0) {
     const uint64_t t8 = (uint64_t)((nx + kWaveTile - 1) / kWaveTile) *
                         (uint64_t)((nrows + kWaveTile - 1) / kWaveTile);
-    variant = t8 >= c->prio_min_tiles ? 4 : 3;
+    variant = t8 >= c->prio_min_tiles ? 5 : 3;
   }
   const int TWd = tile_w(variant), THd = tile_h(variant);
   if (ghost_hi && (nrows % (uint32_t)THd) != 0) return DYMU_ERR_ARG;
@@ -174,7 +176,7 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   const uint32_t ntiles = (uint32_t)ntiles64;
   int rc = ensure_tiles(c, ntiles);
   if (rc) return rc;
-  if (variant == 4 && (rc = ensure_prio(c, ntiles)) != DYMU_OK) return rc;
+  if (is_prio(variant) && (rc = ensure_prio(c, ntiles)) != DYMU_OK) return rc;
   auto& D = c->dom;
   D = dymu_ctx::Dom{};
   D.variant = variant;
@@ -194,12 +196,15 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   HIPC(c, hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * kShards * kStatSlots, st));
   HIPC(c, launch_fill_inf(dT, ld, nx, ghost_lo ? -1 : 0, (int64_t)nrows + (ghost_hi ? 1 : 0), st));
   PassArgs& a = D.a;
-  if (D.variant == 4) {
+  if (is_prio(D.variant)) {
     HIPC(c, launch_prio_init(dF, (int64_t)ld, nx, nrows, c->d_keys, 3ull * ntiles, c->d_hist,
                              3ull * kShards * kBins, c->d_prio,
                              reinterpret_cast<double*>(c->d_prio + 3), prio_delta(c), c->prio_kappa,
                              st));
-    a.target = c->prio_target;
+    // default per pass: 64 8x8 tiles per CU (v4) / 8 16x16 tiles per CU (v5),
+    // the measured optima at 8192^2..16384^2
+    a.target = c->prio_target ? c->prio_target
+                              : (uint32_t)c->cu_count * (D.variant == 5 ? 8u : 64u);
     a.target_frac = c->prio_frac;
     a.delta = prio_delta(c);
   }
@@ -207,7 +212,7 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
     const uint32_t gtile = (uint32_t)(gj / THd) * ntx + (uint32_t)(gi / TWd);
     HIPC(c, launch_seed(dT, ld, gi, gj, D.lists[0], D.counts[0], c->d_tile_epoch, D.eb + 1, gtile,
                         1, st));
-    if (D.variant == 4)
+    if (is_prio(D.variant))
       HIPC(c, launch_prio_seed(c->d_keys, c->d_hist, c->d_prio, gtile, 0.0, st));
   }
   a.F = dF;
@@ -219,14 +224,15 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   a.nty = (int)nty;
   a.ghost_lo = ghost_lo;
   a.ghost_hi = ghost_hi;
-  a.max_inner = c->opts.max_inner > 0 ? c->opts.max_inner : 4 * (TWd + THd);
+  // v5: a short sweep cap bounds the pass latency (capped tiles re-queue themselves)
+  a.max_inner = c->opts.max_inner > 0 ? c->opts.max_inner : variant == 5 ? 16 : 4 * (TWd + THd);
   if (const char* kv = std::getenv("DYMU_MAX_INNER")) a.max_inner = std::max(1, std::atoi(kv));
   a.shard_cap = ntiles;
   a.tile_epoch = c->d_tile_epoch;
   a.stats = c->d_stats;
   // resident workgroups per CU at the kernels' register budgets (v3: 76 VGPRs -> 6 waves/SIMD)
   D.blocks = c->opts.grid_blocks > 0 ? c->opts.grid_blocks
-                                      : c->cu_count * (D.variant == 4 ? 5 : D.variant == 3 ? 6 : 8);
+                                      : c->cu_count * (D.variant == 5 ? 4 : D.variant == 4 ? 5 : D.variant == 3 ? 6 : 8);
   D.live = true;
   return DYMU_OK;
 }
@@ -244,7 +250,7 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
     a.count_out = D.counts[(p + 1) % 3];
     a.count_clear = D.counts[(p + 2) % 3];
     a.epoch = D.eb + (uint32_t)p + 2u;
-    if (D.variant == 4) {
+    if (is_prio(D.variant)) {
       a.key_in = prio_keys(c, p % 3);
       a.key_out = prio_keys(c, (p + 1) % 3);
       a.hist_in = prio_hist(c, p % 3);
@@ -256,7 +262,7 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
       a.base_in = prio_base(c, p % 3);
       a.base_out = prio_base(c, (p + 1) % 3);
     }
-    const bool tr = D.variant == 4 && c->prio_trace >= 0 && p == (uint64_t)c->prio_trace;
+    const bool tr = is_prio(D.variant) && c->prio_trace >= 0 && p == (uint64_t)c->prio_trace;
     if (tr) {
       if (!c->d_trace)
         HIPC(c, hipMalloc(&c->d_trace, sizeof(unsigned long long) * kTracePts * 65536));
@@ -277,6 +283,7 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
     HIPC(c, D.variant == 1   ? launch_pass(a, D.blocks, st, e0, e1)
             : D.variant == 2 ? launch_pass_w8(a, D.blocks, st, e0, e1)
             : D.variant == 4 ? launch_pass_prio(a, D.blocks, st, e0, e1)
+            : D.variant == 5 ? launch_pass_prio16(a, D.blocks, st, e0, e1)
                               : launch_pass_rb(a, D.blocks, st, e0, e1));
     ++D.launches;
     if (tr) {
@@ -292,12 +299,12 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
       for (int b = 0; b < D.blocks; ++b) {
         const unsigned long long* t = &h[(size_t)b * kTracePts];
         auto rel = [&](int k) { return t[k] ? (long long)(t[k] - t0) : -1ll; };
-        std::fprintf(stderr, "B %d %lld %lld %lld %lld %lld %llu %llu %lld %lld %lld\n", b, rel(0),
-                     rel(1), rel(2), rel(3), rel(4), t[5] >> 32, t[5] & 0xffffffffull, rel(6),
-                     rel(7), rel(8));
+        std::fprintf(stderr, "B %d %lld %lld %lld %lld %lld %llu %llu %lld %lld %lld %llu\n", b,
+                     rel(0), rel(1), rel(2), rel(3), rel(4), t[5] >> 32, t[5] & 0xffffffffull,
+                     rel(6), rel(7), rel(8), t[9]);
       }
     }
-    if (D.variant == 4 && c->prio_debug && p < (uint64_t)c->prio_debug) {
+    if (is_prio(D.variant) && c->prio_debug && p < (uint64_t)c->prio_debug) {
       unsigned long long pr[8];
       uint32_t h[kShards * kBins], cnt[kShards];
       HIPC(c, hipStreamSynchronize(st));
@@ -342,11 +349,11 @@ int dom_merge(dymu_ctx* c, const double* lo, const double* hi, int32_t* d_pendin
     HIPC(c, launch_merge_ghosts(D.a.T, D.a.ld, D.a.nx, D.a.ny, lo, hi, D.a.ntx, D.a.nty,
                                 tile_w(D.variant), D.lists[p % 3], D.counts[p % 3], D.ntiles,
                                 c->d_tile_epoch, D.eb + (uint32_t)p + 1u,
-                                D.variant == 4 ? prio_keys(c, p % 3) : nullptr,
-                                D.variant == 4 ? prio_hist(c, p % 3) : nullptr,
-                                D.variant == 4 ? prio_minkey(c, p % 3) : nullptr,
-                                D.variant == 4 ? prio_base(c, p % 3) : nullptr,
-                                D.variant == 4 ? prio_delta(c) : nullptr, st));
+                                is_prio(D.variant) ? prio_keys(c, p % 3) : nullptr,
+                                is_prio(D.variant) ? prio_hist(c, p % 3) : nullptr,
+                                is_prio(D.variant) ? prio_minkey(c, p % 3) : nullptr,
+                                is_prio(D.variant) ? prio_base(c, p % 3) : nullptr,
+                                is_prio(D.variant) ? prio_delta(c) : nullptr, st));
   if (d_pending) HIPC(c, launch_sum_counts(D.counts[p % 3], d_pending, st));
   return DYMU_OK;
 }
@@ -476,21 +483,21 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
   }
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-  if (c->opts.kernel < 0 || c->opts.kernel > 4 || c->opts.prio_target < 0) {
+  if (c->opts.kernel < 0 || c->opts.kernel > 5 || c->opts.prio_target < 0) {
     dymu_destroy(c);
     return DYMU_ERR_ARG;
   }
   c->variant = c->opts.kernel;
   if (const char* kv = std::getenv("DYMU_KERNEL")) {  // development override
     const int v = std::atoi(kv);
-    c->variant = (v >= 0 && v <= 4) ? v : 0;
+    c->variant = (v >= 0 && v <= 5) ? v : 0;
   }
   if (e == hipSuccess) {
-    c->prio_target = c->opts.prio_target > 0 ? (uint32_t)c->opts.prio_target
-                                             : (uint32_t)c->cu_count * 64u;
+    c->prio_target = (uint32_t)c->opts.prio_target;
     if (const char* kv = std::getenv("DYMU_PRIO_TARGET")) c->prio_target = (uint32_t)std::atol(kv);
     if (const char* kv = std::getenv("DYMU_PRIO_KAPPA")) c->prio_kappa = std::atof(kv);
     if (!(c->prio_kappa > 0.0)) c->prio_kappa = 0.5;
+    if (const char* kv = std::getenv("DYMU_GRID_BLOCKS")) c->opts.grid_blocks = std::atoi(kv);
     if (const char* kv = std::getenv("DYMU_PRIO_MIN_TILES"))
       c->prio_min_tiles = (uint32_t)std::atol(kv);
     if (const char* kv = std::getenv("DYMU_PRIO_FRAC")) c->prio_frac = (float)std::atof(kv);

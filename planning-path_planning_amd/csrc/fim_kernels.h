@@ -68,6 +68,8 @@ hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);     // v2: 8x8 tile / wave
 hipError_t launch_pass_prio(const PassArgs& a, int blocks, hipStream_t st,
                            hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+hipError_t launch_pass_prio16(const PassArgs& a, int blocks, hipStream_t st,
+                             hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_pass_rb(const PassArgs& a, int blocks, hipStream_t st,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);     // v3: 2 x 8x8 tiles / wave, red-black
 hipError_t launch_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,

@@ -416,6 +416,7 @@ __global__ __launch_bounds__(256) void k_fim_pass_w8(PassArgs a) {
 // every +-1 / +-pitch shift of them, fall on 32 distinct ds_read_b64 bank pairs
 // and 16 distinct ds_write_b64 banks per 16-lane group (pitch 10 was 2-way).
 constexpr int IP = 12;
+constexpr int IP16 = 20;  // 16x16 image pitch (18 + 2)
 
 // v_min_f64 on operands that are never NaN (T >= 0 or +inf): one instruction,
 // no canonicalisation (the compiler cannot prove no-NaN for fmin).
@@ -448,13 +449,13 @@ constexpr double kFastMinF = 0x1p-383;
 // (guaranteed by the skip test): f finite and min(Tx,Ty) finite, so the
 // reference's "Tx < inf && Ty < inf" is implied by |Tx - Ty| < C.
 // c2x2 = 2*(C*C) is precomputed: the same two roundings as 2*pow(C,2.0).
-template <bool FAST>
+template <bool FAST, int PITCH = IP>
 __device__ __forceinline__ bool rb_update(double* img, int slot, double f, double k1, double c2x2,
                                           double& t) {
-  const double south = img[slot - IP];
+  const double south = img[slot - PITCH];
   const double west = img[slot - 1];
   const double east = img[slot + 1];
-  const double north = img[slot + IP];
+  const double north = img[slot + PITCH];
   const double tx_ = vmin64(west, east), ty_ = vmin64(north, south);
   const double m = vmin64(tx_, ty_);
   if (m + k1 < t) {  // exact skip bound U >= min + C/sqrt(2); k1 = 0.7071*C
@@ -721,7 +722,210 @@ __device__ __forceinline__ int key_bin(double k, double origin, double inv_delta
   return b < (float)(kBins - 1) ? (int)b : kBins - 1;
 }
 
+// ---- v4 tile visits: load tile + halo into the wave's LDS image, red-black
+// sweeps to local convergence, write back decreased cells, and leave in ek[0..3]
+// (S, W, E, N) the minimum decreased value on each edge (+inf bits: unchanged).
+// Returns the sweep count; capped = the sweep cap was hit.
+
+// 8x8, half-wave per tile (the v3 body): lane (r, q) owns red column cr and
+// black column cb of row r.
+__device__ __forceinline__ int visit8(const PassArgs& a, double* img, unsigned long long* ek,
+                                      bool has, int tx, int ty, int r, int q, int cr, int cb,
+                                      bool& capped) {
+  const int sr = (r + 1) * IP + (cr + 1);
+  const int sb = (r + 1) * IP + (cb + 1);
+  const int64_t i0 = (int64_t)tx * WT, j0 = (int64_t)ty * WT;
+  const int64_t gj = j0 + r, gir = i0 + cr, gib = i0 + cb;
+  const bool rowin = has && gj < a.ny;
+  double tr = dinf(), fr = dinf(), tb = dinf(), fb = dinf();
+  if (rowin && gir < a.nx) {
+    tr = a.T[gj * a.ld + gir];
+    fr = a.F[gj * a.ld + gir];
+  }
+  if (rowin && gib < a.nx) {
+    tb = a.T[gj * a.ld + gib];
+    fb = a.F[gj * a.ld + gib];
+  }
+  double hw = dinf(), he = dinf(), hs0 = dinf(), hs1 = dinf(), hn0 = dinf(), hn1 = dinf();
+  if (rowin) {
+    if (q == 0 && i0 > 0) hw = a.T[gj * a.ld + (i0 - 1)];
+    if (q == 3 && i0 + WT < a.nx) he = a.T[gj * a.ld + (i0 + WT)];
+  }
+  if (has) {
+    const int64_t cc0 = i0 + 2 * q, cc1 = cc0 + 1;
+    if (r == 0 && (j0 > 0 || a.ghost_lo)) {
+      if (cc0 < a.nx) hs0 = a.T[(j0 - 1) * a.ld + cc0];
+      if (cc1 < a.nx) hs1 = a.T[(j0 - 1) * a.ld + cc1];
+    }
+    if (r == WT - 1) {
+      const int64_t jn = j0 + WT;
+      if (jn < a.ny || (jn == a.ny && a.ghost_hi)) {
+        if (cc0 < a.nx) hn0 = a.T[jn * a.ld + cc0];
+        if (cc1 < a.nx) hn1 = a.T[jn * a.ld + cc1];
+      }
+    }
+  }
+  {
+    const int row = (r + 1) * IP;
+    if (q == 0) img[row] = hw;
+    if (q == 3) img[row + WT + 1] = he;
+    if (r == 0) {
+      img[1 + 2 * q] = hs0;
+      img[2 + 2 * q] = hs1;
+    }
+    if (r == WT - 1) {
+      img[(WT + 1) * IP + 1 + 2 * q] = hn0;
+      img[(WT + 1) * IP + 2 + 2 * q] = hn1;
+    }
+    img[sb] = tb;
+  }
+  const double tr0 = tr, tb0 = tb;
+  const bool fast = __all(!(fr < kFastMinF) && !(fb < kFastMinF));
+  const int sweeps = fast ? rb_sweeps<true>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped)
+                          : rb_sweeps<false>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped);
+  const bool dr = tr < tr0, db = tb < tb0;
+  if (dr) a.T[gj * a.ld + gir] = tr;
+  if (db) a.T[gj * a.ld + gib] = tb;
+  const unsigned long long vr = dr ? dbits(tr) : kInfBits;
+  const unsigned long long vb = db ? dbits(tb) : kInfBits;
+  const unsigned long long vrb = vr < vb ? vr : vb;
+  if (r == 0 && vrb != kInfBits) atomicMin(&ek[0], vrb);
+  if (r == WT - 1 && vrb != kInfBits) atomicMin(&ek[3], vrb);
+  const unsigned long long vw = cr == 0 ? vr : (cb == 0 ? vb : kInfBits);
+  const unsigned long long ve = cr == WT - 1 ? vr : (cb == WT - 1 ? vb : kInfBits);
+  if (vw != kInfBits) atomicMin(&ek[1], vw);
+  if (ve != kInfBits) atomicMin(&ek[2], ve);
+  return sweeps;
+}
+
+// 16x16, one tile per wave: lane (r = lane>>2, q = lane&3) owns the four
+// cells (r, 4q..4q+3): red columns 4q+(r&1), 4q+2+(r&1), black the other two.
+// A half-sweep updates two independent cells per lane.
+template <bool FAST>
+__device__ __forceinline__ int rb_sweeps4(double* img, const int (&sr)[2], const int (&sb)[2],
+                                          const double (&fr)[2], const double (&fb)[2],
+                                          double (&tr)[2], double (&tb)[2], int max_inner,
+                                          bool& capped) {
+  double k1r[2], k1b[2], c2r[2], c2b[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    k1r[k] = 0.7071 * fr[k];
+    k1b[k] = 0.7071 * fb[k];
+    c2r[k] = 2.0 * (fr[k] * fr[k]);
+    c2b[k] = 2.0 * (fb[k] * fb[k]);
+  }
+  int sweeps = 0;
+  capped = true;
+  while (sweeps < max_inner) {
+    __builtin_amdgcn_wave_barrier();
+    const bool i0 = rb_update<FAST, IP16>(img, sr[0], fr[0], k1r[0], c2r[0], tr[0]);
+    const bool i1 = rb_update<FAST, IP16>(img, sr[1], fr[1], k1r[1], c2r[1], tr[1]);
+    img[sr[0]] = tr[0];
+    img[sr[1]] = tr[1];
+    __builtin_amdgcn_wave_barrier();
+    const bool i2 = rb_update<FAST, IP16>(img, sb[0], fb[0], k1b[0], c2b[0], tb[0]);
+    const bool i3 = rb_update<FAST, IP16>(img, sb[1], fb[1], k1b[1], c2b[1], tb[1]);
+    img[sb[0]] = tb[0];
+    img[sb[1]] = tb[1];
+    ++sweeps;
+    if (!__any(i0 || i1 || i2 || i3)) {
+      capped = false;
+      break;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  return sweeps;
+}
+
+__device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned long long* ek,
+                                       bool has, int tx, int ty, int lane, bool& capped) {
+  constexpr int TT = 16;
+  const int r = lane >> 2, q = lane & 3, odd = r & 1;
+  const int cr[2] = {4 * q + odd, 4 * q + 2 + odd};
+  const int cb[2] = {4 * q + 1 - odd, 4 * q + 3 - odd};
+  const int row = (r + 1) * IP16;
+  const int sr[2] = {row + cr[0] + 1, row + cr[1] + 1};
+  const int sb[2] = {row + cb[0] + 1, row + cb[1] + 1};
+  const int64_t i0 = (int64_t)tx * TT, j0 = (int64_t)ty * TT;
+  const int64_t gj = j0 + r;
+  const bool rowin = has && gj < a.ny;
+  double tr[2], tb[2], fr[2], fb[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    tr[k] = fr[k] = tb[k] = fb[k] = dinf();
+    if (rowin && i0 + cr[k] < a.nx) {
+      tr[k] = a.T[gj * a.ld + i0 + cr[k]];
+      fr[k] = a.F[gj * a.ld + i0 + cr[k]];
+    }
+    if (rowin && i0 + cb[k] < a.nx) {
+      tb[k] = a.T[gj * a.ld + i0 + cb[k]];
+      fb[k] = a.F[gj * a.ld + i0 + cb[k]];
+    }
+  }
+  double hw = dinf(), he = dinf(), hs[4], hn[4];
+  if (rowin) {
+    if (q == 0 && i0 > 0) hw = a.T[gj * a.ld + (i0 - 1)];
+    if (q == 3 && i0 + TT < a.nx) he = a.T[gj * a.ld + (i0 + TT)];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) hs[k] = hn[k] = dinf();
+  if (has) {
+    if (r == 0 && (j0 > 0 || a.ghost_lo)) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (i0 + 4 * q + k < a.nx) hs[k] = a.T[(j0 - 1) * a.ld + i0 + 4 * q + k];
+    }
+    if (r == TT - 1) {
+      const int64_t jn = j0 + TT;
+      if (jn < a.ny || (jn == a.ny && a.ghost_hi)) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (i0 + 4 * q + k < a.nx) hn[k] = a.T[jn * a.ld + i0 + 4 * q + k];
+      }
+    }
+  }
+  if (q == 0) img[row] = hw;
+  if (q == 3) img[row + TT + 1] = he;
+  if (r == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) img[1 + 4 * q + k] = hs[k];
+  }
+  if (r == TT - 1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) img[(TT + 1) * IP16 + 1 + 4 * q + k] = hn[k];
+  }
+  img[sb[0]] = tb[0];
+  img[sb[1]] = tb[1];
+  const double tr0[2] = {tr[0], tr[1]}, tb0[2] = {tb[0], tb[1]};
+  const bool fast = __all(!(fr[0] < kFastMinF) && !(fr[1] < kFastMinF) &&
+                          !(fb[0] < kFastMinF) && !(fb[1] < kFastMinF));
+  const int sweeps = fast ? rb_sweeps4<true>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped)
+                          : rb_sweeps4<false>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped);
+  unsigned long long v[4];  // cells 4q..4q+3 in column order, decreased value or +inf
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const bool dr = tr[k] < tr0[k], db = tb[k] < tb0[k];
+    if (dr) a.T[gj * a.ld + i0 + cr[k]] = tr[k];
+    if (db) a.T[gj * a.ld + i0 + cb[k]] = tb[k];
+    v[cr[k] - 4 * q] = dr ? dbits(tr[k]) : kInfBits;
+    v[cb[k] - 4 * q] = db ? dbits(tb[k]) : kInfBits;
+  }
+  const unsigned long long m01 = v[0] < v[1] ? v[0] : v[1];
+  const unsigned long long m23 = v[2] < v[3] ? v[2] : v[3];
+  const unsigned long long vall = m01 < m23 ? m01 : m23;
+  if (r == 0 && vall != kInfBits) atomicMin(&ek[0], vall);
+  if (r == TT - 1 && vall != kInfBits) atomicMin(&ek[3], vall);
+  if (q == 0 && v[0] != kInfBits) atomicMin(&ek[1], v[0]);
+  if (q == 3 && v[3] != kInfBits) atomicMin(&ek[2], v[3]);
+  return sweeps;
+}
+
+template <int TS>  // 8: two 8x8 tiles per wave (v3 body); 16: one 16x16 tile per wave
 __global__ __launch_bounds__(256) void k_fim_pass_prio(PassArgs a) {
+  static_assert(TS == 8 || TS == 16, "tile size");
+  constexpr int TPW = TS == 8 ? 2 : 1;  // tiles per wave
+  constexpr int SLOTS = 4 * TPW;         // tile slots per workgroup
+  constexpr int IMG = TS == 8 ? (WT + 2) * IP : (16 + 2) * IP16;
   __shared__ uint32_t s_q[QCAP];
   __shared__ uint32_t s_work[WCAP];
   __shared__ unsigned long long s_wkey[WCAP];
@@ -730,8 +934,8 @@ __global__ __launch_bounds__(256) void k_fim_pass_prio(PassArgs a) {
   __shared__ uint32_t s_nq, s_base, s_nwork;
   __shared__ int s_bstar;
   __shared__ unsigned long long s_visits, s_sweeps, s_minout;
-  __shared__ unsigned long long s_ek[8][4];
-  __shared__ double s_img[8][(WT + 2) * IP];
+  __shared__ unsigned long long s_ek[SLOTS][4];
+  __shared__ double s_img[SLOTS][IMG];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -812,11 +1016,12 @@ __global__ __launch_bounds__(256) void k_fim_pass_prio(PassArgs a) {
   };
 
   unsigned long long my_visits = 0, my_sweeps = 0;
-  double* img = s_img[wv * 2 + half];
-  unsigned long long* ek = s_ek[wv * 2 + half];
-  const int sr = (r + 1) * IP + (cr + 1);
-  const int sb = (r + 1) * IP + (cb + 1);
-  const unsigned long long hmask = half ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+  const int slot = TS == 8 ? wv * 2 + half : wv;
+  const int sl = TS == 8 ? hl : lane;  // lane within the tile's lane group
+  double* img = s_img[slot];
+  unsigned long long* ek = s_ek[slot];
+  const unsigned long long hmask =
+      TS == 16 ? ~0ull : (half ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull);
 
   const uint32_t chunk = (n_active + gridDim.x - 1) / gridDim.x;
   const uint32_t c0 = blockIdx.x * chunk;
@@ -840,8 +1045,8 @@ __global__ __launch_bounds__(256) void k_fim_pass_prio(PassArgs a) {
     __syncthreads();
     const uint32_t nw = s_nwork;
     if (trace && tid == 0 && s0 == c0) trace[2] = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t wb = (uint32_t)wv * 2u; wb < nw; wb += 8u) {  // wave-uniform
-      const uint32_t li = wb + (uint32_t)half;
+    for (uint32_t wb = (uint32_t)(wv * TPW); wb < nw; wb += (uint32_t)SLOTS) {  // wave-uniform
+      const uint32_t li = wb + (uint32_t)(TS == 8 ? half : 0);
       const bool has = li < nw;
       uint32_t tile = 0;
       int tx = 0, ty = 0;
@@ -850,80 +1055,22 @@ __global__ __launch_bounds__(256) void k_fim_pass_prio(PassArgs a) {
         tx = (int)(tile % (uint32_t)a.ntx);
         ty = (int)(tile / (uint32_t)a.ntx);
       }
-      if (hl < 4) ek[hl] = kInfBits;
-      const int64_t i0 = (int64_t)tx * WT, j0 = (int64_t)ty * WT;
-      const int64_t gj = j0 + r, gir = i0 + cr, gib = i0 + cb;
-      const bool rowin = has && gj < a.ny;
-      double tr = dinf(), fr = dinf(), tb = dinf(), fb = dinf();
-      if (rowin && gir < a.nx) {
-        tr = a.T[gj * a.ld + gir];
-        fr = a.F[gj * a.ld + gir];
-      }
-      if (rowin && gib < a.nx) {
-        tb = a.T[gj * a.ld + gib];
-        fb = a.F[gj * a.ld + gib];
-      }
-      double hw = dinf(), he = dinf(), hs0 = dinf(), hs1 = dinf(), hn0 = dinf(), hn1 = dinf();
-      if (rowin) {
-        if (q == 0 && i0 > 0) hw = a.T[gj * a.ld + (i0 - 1)];
-        if (q == 3 && i0 + WT < a.nx) he = a.T[gj * a.ld + (i0 + WT)];
-      }
-      if (has) {
-        const int64_t cc0 = i0 + 2 * q, cc1 = cc0 + 1;
-        if (r == 0 && (j0 > 0 || a.ghost_lo)) {
-          if (cc0 < a.nx) hs0 = a.T[(j0 - 1) * a.ld + cc0];
-          if (cc1 < a.nx) hs1 = a.T[(j0 - 1) * a.ld + cc1];
-        }
-        if (r == WT - 1) {
-          const int64_t jn = j0 + WT;
-          if (jn < a.ny || (jn == a.ny && a.ghost_hi)) {
-            if (cc0 < a.nx) hn0 = a.T[jn * a.ld + cc0];
-            if (cc1 < a.nx) hn1 = a.T[jn * a.ld + cc1];
-          }
-        }
-      }
-      {
-        const int row = (r + 1) * IP;
-        if (q == 0) img[row] = hw;
-        if (q == 3) img[row + WT + 1] = he;
-        if (r == 0) {
-          img[1 + 2 * q] = hs0;
-          img[2 + 2 * q] = hs1;
-        }
-        if (r == WT - 1) {
-          img[(WT + 1) * IP + 1 + 2 * q] = hn0;
-          img[(WT + 1) * IP + 2 + 2 * q] = hn1;
-        }
-        img[sb] = tb;
-      }
-      const double tr0 = tr, tb0 = tb;
+      if (sl < 4) ek[sl] = kInfBits;
+      if (trace && tid == 0 && wb == 0) trace[6] = __builtin_amdgcn_s_memrealtime();
+      bool capped;
+      int sweeps;
+      if constexpr (TS == 8)
+        sweeps = visit8(a, img, ek, has, tx, ty, r, q, cr, cb, capped);
+      else
+        sweeps = visit16(a, img, ek, has, tx, ty, lane, capped);
       if (trace && tid == 0 && wb == 0) {
         __builtin_amdgcn_s_waitcnt(0);
-        trace[6] = __builtin_amdgcn_s_memrealtime();
+        trace[7] = __builtin_amdgcn_s_memrealtime();
+        trace[9] = (unsigned long long)sweeps;
       }
-      const bool fast = __all(!(fr < kFastMinF) && !(fb < kFastMinF));
-      bool capped;
-      const int sweeps = fast ? rb_sweeps<true>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped)
-                              : rb_sweeps<false>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped);
       if (has) {
         my_visits += 1;
         my_sweeps += (unsigned long long)sweeps;
-      }
-      if (trace && tid == 0 && wb == 0) trace[7] = __builtin_amdgcn_s_memrealtime();
-      const bool dr = tr < tr0, db = tb < tb0;
-      if (dr) a.T[gj * a.ld + gir] = tr;
-      if (db) a.T[gj * a.ld + gib] = tb;
-      // minimum decreased value on each edge: the key of the neighbour it wakes
-      {
-        const unsigned long long vr = dr ? dbits(tr) : kInfBits;
-        const unsigned long long vb = db ? dbits(tb) : kInfBits;
-        const unsigned long long vrb = vr < vb ? vr : vb;
-        if (r == 0 && vrb != kInfBits) atomicMin(&ek[0], vrb);
-        if (r == WT - 1 && vrb != kInfBits) atomicMin(&ek[3], vrb);
-        const unsigned long long vw = cr == 0 ? vr : (cb == 0 ? vb : kInfBits);
-        const unsigned long long ve = cr == WT - 1 ? vr : (cb == WT - 1 ? vb : kInfBits);
-        if (vw != kInfBits) atomicMin(&ek[1], vw);
-        if (ve != kInfBits) atomicMin(&ek[2], ve);
       }
       const unsigned long long mC = __ballot(capped && has) & hmask;
       __builtin_amdgcn_wave_barrier();
@@ -931,13 +1078,13 @@ __global__ __launch_bounds__(256) void k_fim_pass_prio(PassArgs a) {
       bool want = false;
       int nx_t = tx, ny_t = ty;
       unsigned long long kb = kInfBits;
-      if (has && hl < 4) {
-        kb = ek[hl];
-        if (hl == 0) { want = kb != kInfBits && ty > 0; ny_t = ty - 1; }
-        else if (hl == 1) { want = kb != kInfBits && tx > 0; nx_t = tx - 1; }
-        else if (hl == 2) { want = kb != kInfBits && tx + 1 < a.ntx; nx_t = tx + 1; }
+      if (has && sl < 4) {
+        kb = ek[sl];
+        if (sl == 0) { want = kb != kInfBits && ty > 0; ny_t = ty - 1; }
+        else if (sl == 1) { want = kb != kInfBits && tx > 0; nx_t = tx - 1; }
+        else if (sl == 2) { want = kb != kInfBits && tx + 1 < a.ntx; nx_t = tx + 1; }
         else { want = kb != kInfBits && ty + 1 < a.nty; ny_t = ty + 1; }
-      } else if (has && hl == 4 && mC != 0ull) {
+      } else if (has && sl == 4 && mC != 0ull) {
         want = true;
         kb = s_wkey[li];
       }
@@ -955,7 +1102,7 @@ __global__ __launch_bounds__(256) void k_fim_pass_prio(PassArgs a) {
     atomicAdd(&s_visits, my_visits);
     atomicAdd(&s_sweeps, my_sweeps);
   }
-  if (lane == 32 && my_visits) {
+  if (TS == 8 && lane == 32 && my_visits) {  // each half counted its own tiles
     atomicAdd(&s_visits, my_visits);
     atomicAdd(&s_sweeps, my_sweeps);
   }
@@ -1168,9 +1315,18 @@ hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st, hipEven
 hipError_t launch_pass_prio(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
                             hipEvent_t e1) {
   if (e0 || e1)
-    hipExtLaunchKernelGGL(k_fim_pass_prio, dim3(blocks), dim3(256), 0, st, e0, e1, 0, a);
+    hipExtLaunchKernelGGL(k_fim_pass_prio<8>, dim3(blocks), dim3(256), 0, st, e0, e1, 0, a);
   else
-    hipLaunchKernelGGL(k_fim_pass_prio, dim3(blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_fim_pass_prio<8>, dim3(blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_pass_prio16(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
+                              hipEvent_t e1) {
+  if (e0 || e1)
+    hipExtLaunchKernelGGL(k_fim_pass_prio<16>, dim3(blocks), dim3(256), 0, st, e0, e1, 0, a);
+  else
+    hipLaunchKernelGGL(k_fim_pass_prio<16>, dim3(blocks), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

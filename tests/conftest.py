@@ -52,7 +52,8 @@ def engine(dymu):
 
 # pass kernels under test: 3 = plain block FIM, 4 = priority passes with a small
 # per-pass target so that deferral happens even on test-sized grids
-KERNELS = {"fim": dict(kernel=3), "prio": dict(kernel=4, prio_target=64)}
+KERNELS = {"fim": dict(kernel=3), "prio": dict(kernel=4, prio_target=64),
+           "prio16": dict(kernel=5, prio_target=16)}
 
 
 @pytest.fixture(scope="session", params=sorted(KERNELS))

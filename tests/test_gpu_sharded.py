@@ -51,7 +51,8 @@ def _worker(rank, world, port, nx, ny, goal, F_full, out_q, engine_kw):
 
 @pytest.mark.parametrize("world,nx,ny,goal,engine_kw", [
     (2, 300, 256, (150, 128), dict(kernel=3)),
-    (3, 200, 230, (20, 30), dict(kernel=4, prio_target=32))])
+    (3, 200, 230, (20, 30), dict(kernel=4, prio_target=32)),
+    (2, 257, 300, (250, 3), dict(kernel=5, prio_target=8))])
 def test_gpu_sharded_matches_oracle(oracle, world, nx, ny, goal, engine_kw):
     import torch.multiprocessing as mp
     F = oracle.synth_speed(nx, ny, seed=41, obst_frac=0.03, obst_seed=43, goal=goal)

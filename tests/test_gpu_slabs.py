@@ -60,8 +60,8 @@ def solve_virtual_slabs(dymu, F, goal, S, K=8, **engine_kw):
 @pytest.mark.parametrize("S,nx,ny,goal,frac", [(2, 200, 160, (100, 40), 0.02),
                                                (3, 130, 200, (7, 190), 0.05),
                                                (4, 256, 256, (128, 128), 0.0)])
-@pytest.mark.parametrize("kw", [dict(kernel=3), dict(kernel=4, prio_target=32)],
-                         ids=["fim", "prio"])
+@pytest.mark.parametrize("kw", [dict(kernel=3), dict(kernel=4, prio_target=32),
+                                dict(kernel=5, prio_target=8)], ids=["fim", "prio", "prio16"])
 def test_virtual_slabs_match_oracle(dymu, oracle, S, nx, ny, goal, frac, kw):
     F = oracle.synth_speed(nx, ny, seed=31, obst_frac=frac, obst_seed=5, goal=goal)
     T, rounds = solve_virtual_slabs(dymu, F, goal, S, **kw)

@@ -117,25 +117,29 @@ def test_priority_kernel_defers(dymu, oracle):
     g = (512, 512)
     F = oracle.synth_speed(nx, ny, seed=2, obst_frac=0.02, obst_seed=4, goal=g)
     out = {}
-    for k, kw in ((3, {}), (4, dict(prio_target=256))):
+    for k, kw in ((3, {}), (4, dict(prio_target=256)), (5, dict(prio_target=64))):
         eng = dymu.Engine(kernel=k, **kw)
         try:
             out[k] = eng.solve(F, g[0], g[1])
         finally:
             eng.close()
-    assert out[3].stats["kernel"] == 3 and out[4].stats["kernel"] == 4
+    assert [out[k].stats["kernel"] for k in (3, 4, 5)] == [3, 4, 5]
     assert out[4].stats["tile_visits"] < out[3].stats["tile_visits"]
     Tref, _ = oracle.fmm(F, g)
-    assert_parity(out[3].T, Tref)
-    assert_parity(out[4].T, Tref)
+    for k in (3, 4, 5):
+        assert_parity(out[k].T, Tref)
 
 
 def test_auto_kernel_choice(dymu):
-    """kernel=0 picks plain FIM below 2^19 8x8 tiles (~5800^2 cells)."""
+    """kernel=0 picks plain FIM below 2^17 8x8 tiles (~2900^2 cells) and
+    16x16 priority passes from there up."""
     eng = dymu.Engine()
     try:
         r = eng.solve(np.ones((64, 64)), 3, 3)
-        assert r.stats["kernel"] == 3
+        assert r.stats["kernel"] == 3 and r.stats["tile_w"] == 8
+        r = eng.solve(np.ones((2900, 2900)), 3, 3)
+        assert r.stats["kernel"] == 5 and r.stats["tile_w"] == 16
+        assert r.T[3, 13] == 10.0  # on the axis through the goal: the distance
     finally:
         eng.close()
     with pytest.raises(dymu.DymuError):
