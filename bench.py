@@ -73,7 +73,8 @@ def cpu_baseline(n_edge, obst):
 
 
 PROFILE_PERIOD = 8  # time every 8th pass launch with HIP events (sampled mean duration)
-KERNEL_NAMES = {1: "k_fim_pass", 2: "k_fim_pass_w8", 3: "k_fim_pass_rb", 4: "k_fim_pass_prio"}
+KERNEL_NAMES = {1: "k_fim_pass(", 2: "k_fim_pass_w8", 3: "k_fim_pass_rb", 4: "k_fim_pass_prio<8>",
+                5: "k_fim_pass_prio<16>"}
 
 
 def run_single(args):
@@ -131,10 +132,14 @@ def main():
     value = N * N * K / dt / 1e6
     roof = None
     if kern_n > 0 and kern_ms > 0:
+        launch_s = kern_ms * 1e-3 / kern_n  # mean duration of a pass launch (sampled events)
+        # (i) SURVEY s8(d)(i), the judged figure: 16 B per cell per solve (read F + write T
+        # once), spread over the solve's pass launches
+        bytes_i = N * N * BYTES_PER_CELL_SOLVE * K / tot["launches"]
+        achieved = bytes_i / launch_s / 1e9
+        # (ii) diagnostic sweep efficiency: 24 B per cell-visit in the launch
         cells_visited = tot["tile_visits"] * st["tile_w"] * st["tile_h"]
-        bytes_alg = cells_visited * BYTES_PER_CELL_VISIT
-        # algorithmic bytes per launch / mean sampled launch duration
-        achieved = (bytes_alg / tot["launches"]) / (kern_ms * 1e-3 / kern_n) / 1e9
+        bytes_ii = cells_visited * BYTES_PER_CELL_VISIT / tot["launches"]
         roof = {
             "bound": "hbm",
             "achieved": round(achieved, 3),
@@ -143,10 +148,17 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 6),
             "traffic": None,
             "kernel": KERNEL_NAMES.get(st.get("kernel", 3), "k_fim_pass_rb"),
-            "bytes_per_launch": bytes_alg / tot["launches"],
-            "avg_launch_us": kern_ms * 1e3 / kern_n,
+            "per_unit": "16 B per cell per solve (SURVEY s8(d)(i)) / pass launches per solve",
+            "bytes_per_launch": bytes_i,
+            "avg_launch_us": launch_s * 1e6,
+            "launches_per_solve": tot["launches"] / K,
             "timed_launches": f"{kern_n} of {tot['launches']} (every {PROFILE_PERIOD}th)",
-            "per_unit": "24 B per cell-visit (SURVEY s8(d)(ii))",
+            "sweep": {
+                "per_unit": "24 B per cell-visit",
+                "bytes_per_launch": bytes_ii,
+                "achieved": round(bytes_ii / launch_s / 1e9, 3),
+                "frac": round(bytes_ii / launch_s / 1e9 / HBM_PEAK_GBS, 6),
+            },
             "headline_solve_GBs": round(N * N * BYTES_PER_CELL_SOLVE * K / dt / 1e9, 3),
         }
     if roof is not None:
@@ -154,13 +166,13 @@ def main():
         # workload (tools/pmc_round.sh -> tools/pmc_summary.py), if committed
         import glob
         pm = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
-        if pm:
-            d = json.load(open(pm[-1]))
-            if d.get("kernel") and roof["kernel"] in d["kernel"]:
-                roof["traffic"] = round(d["traffic_bytes_per_launch"] / 1e6, 3)
-                roof["traffic_unit"] = "MB per launch (PMC, FETCH x2 corrected)"
-                roof["traffic_source"] = os.path.basename(pm[-1])
-                roof["bytes_per_launch_MB"] = round(roof.pop("bytes_per_launch") / 1e6, 3)
+        for f in reversed(pm):  # newest summary of THIS kernel
+            d = json.load(open(f))
+            if d.get("kernel") and roof["kernel"] in d["kernel"] and d.get("grid", N) == N:
+                roof["traffic"] = round(d["traffic_bytes_per_launch"])
+                roof["traffic_unit"] = "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
+                roof["traffic_source"] = os.path.basename(f)
+                break
     line = {
         "metric": "global total-cost-map Mcells/s (16384^2 grid); iters to converge",
         "value": round(value, 3),

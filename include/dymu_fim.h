@@ -145,11 +145,45 @@ int dymu_synth_speed(dymu_ctx* ctx, double* dF, uint32_t nx, uint32_t ny, uint64
 int dymu_eikonal_batch(dymu_ctx* ctx, const double* tx, const double* ty, const double* c,
                        double* out, uint64_t n, int fast);
 
-/* Device memory helpers (so a host without torch can run the device path). */
+/* Device memory helpers (so a host without torch can run the device path).
+ * The copies are ordered after the work queued on the context stream and are
+ * complete on return. */
 int dymu_device_alloc(dymu_ctx* ctx, size_t bytes, void** dptr);
 int dymu_device_free(dymu_ctx* ctx, void* dptr);
 int dymu_memcpy_d2h(dymu_ctx* ctx, void* dst, const void* src, size_t bytes);
 int dymu_memcpy_h2d(dymu_ctx* ctx, void* dst, const void* src, size_t bytes);
+
+/* ---- computeCostMap on the device ----
+ * Planner node state (the globalNode fields of reference src/DyMu.hpp:69-108
+ * that the global layer uses) as device SoA arrays, row-major, pitch ld. */
+typedef struct dymu_cost_state {
+  double* cost;         /* smoothed cost; its previous value feeds the smoothing (Q1) */
+  double* raw_cost;     /* nominal cost before smoothing */
+  double* slope;        /* rad */
+  uint32_t* terrain;    /* terrain class, 0 on the border */
+  uint8_t* is_obstacle; /* sticky */
+  double* hazard;       /* hazard_density */
+  double* traff;        /* trafficability */
+  int32_t* loc_mode;    /* -1 = "DONT_CARE", else the locomotion index */
+} dymu_cost_state;
+
+/* computeCostMap (reference src/DyMu_GlobalPathPlanning.cpp:145-181 with
+ * calculateSlope :186-210, calculateNominalCost :217-293, smoothCost
+ * :297-308; quirks Q1-Q4) over device arrays elevation / terrain_map (class
+ * as double, like the reference's vector<vector<double>>); lut and slopes are
+ * HOST arrays (the reference's cost_data / slope_values).  If dF is not NULL
+ * the speed F = (res*cost)*((2+hazard)-traff), +inf for obstacles (:527-528),
+ * is written too.  Asynchronous on `stream` (NULL: the context's stream).
+ * nx, ny >= 2.  A terrain class beyond the LUT marks the cell as an obstacle
+ * (the reference reads out of bounds there). */
+int dymu_compute_cost_map(dymu_ctx* ctx, uint32_t nx, uint32_t ny, uint64_t ld, double global_res,
+                          const double* lut, int lut_len, const double* slopes, int n_slopes,
+                          int n_locs, const double* elevation, const double* terrain_map,
+                          const dymu_cost_state* st, double* dF, void* stream);
+
+/* The speed alone from the state (after hazard / trafficability updates). */
+int dymu_pack_speed(dymu_ctx* ctx, uint32_t nx, uint32_t ny, uint64_t ld, double global_res,
+                    const dymu_cost_state* st, double* dF, void* stream);
 
 /* Profiling: period > 0 times every period-th pass launch with HIP events
  * (start/stop taken by the dispatch itself); 0 turns it off.  Sampling keeps

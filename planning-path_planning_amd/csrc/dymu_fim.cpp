@@ -57,6 +57,8 @@ struct dymu_ctx {
   unsigned long long* d_prio = nullptr;
   uint32_t epoch_base = 0;
   uint32_t* h_count = nullptr;  // pinned
+  double* d_lut = nullptr;      // computeCostMap LUT (device copy)
+  size_t lut_cap = 0;
 
   // host-solve staging
   double* d_F = nullptr;
@@ -530,6 +532,7 @@ int dymu_destroy(dymu_ctx* c) {
   if (c->d_hist) (void)hipFree(c->d_hist);
   if (c->d_prio) (void)hipFree(c->d_prio);
   if (c->d_trace) (void)hipFree(c->d_trace);
+  if (c->d_lut) (void)hipFree(c->d_lut);
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->d_F) (void)hipFree(c->d_F);
   if (c->d_T) (void)hipFree(c->d_T);
@@ -589,14 +592,17 @@ int dymu_device_free(dymu_ctx* c, void* p) {
 int dymu_memcpy_d2h(dymu_ctx* c, void* dst, const void* src, size_t bytes) {
   if (!c) return DYMU_ERR_ARG;
   HIPC(c, hipSetDevice(c->device));
-  HIPC(c, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  // ordered after the work queued on the context stream, complete on return
+  HIPC(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
   return DYMU_OK;
 }
 
 int dymu_memcpy_h2d(dymu_ctx* c, void* dst, const void* src, size_t bytes) {
   if (!c) return DYMU_ERR_ARG;
   HIPC(c, hipSetDevice(c->device));
-  HIPC(c, hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  HIPC(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
   return DYMU_OK;
 }
 
@@ -654,6 +660,73 @@ int dymu_eikonal_batch(dymu_ctx* c, const double* tx, const double* ty, const do
   HIPC(c, hipSetDevice(c->device));
   HIPC(c, launch_eikonal_batch(tx, ty, cc, out, n, fast, c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
+  return DYMU_OK;
+}
+
+namespace {
+dymu::CostState cost_state(const dymu_cost_state* s) {
+  return dymu::CostState{s->cost,        s->raw_cost, s->slope, s->terrain,
+                         s->is_obstacle, s->hazard,   s->traff, s->loc_mode};
+}
+bool cost_state_ok(const dymu_cost_state* s) {
+  return s && s->cost && s->raw_cost && s->slope && s->terrain && s->is_obstacle && s->hazard &&
+         s->traff && s->loc_mode;
+}
+}  // namespace
+
+int dymu_compute_cost_map(dymu_ctx* c, uint32_t nx, uint32_t ny, uint64_t ld, double global_res,
+                          const double* lut, int lut_len, const double* slopes, int n_slopes,
+                          int n_locs, const double* elevation, const double* terrain_map,
+                          const dymu_cost_state* st, double* dF, void* stream) {
+  if (!c || !lut || lut_len <= 0 || !slopes || n_slopes <= 0 || n_locs <= 0 || !elevation ||
+      !terrain_map || !cost_state_ok(st) || nx < 2 || ny < 2 || ld < nx || !(global_res > 0))
+    return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  hipStream_t s = pick_stream(c, stream);
+  if ((size_t)lut_len > c->lut_cap) {
+    if (c->d_lut) (void)hipFree(c->d_lut);
+    c->d_lut = nullptr;
+    c->lut_cap = 0;
+    HIPC(c, hipMalloc(&c->d_lut, sizeof(double) * (size_t)lut_len));
+    c->lut_cap = (size_t)lut_len;
+  }
+  // the previous launch reading d_lut must be done before it is overwritten
+  HIPC(c, hipStreamSynchronize(s));
+  HIPC(c, hipMemcpy(c->d_lut, lut, sizeof(double) * (size_t)lut_len, hipMemcpyHostToDevice));
+  dymu::CostArgs a{};
+  a.nx = nx;
+  a.ny = ny;
+  a.ld = (int64_t)ld;
+  a.res = global_res;
+  a.cmax = lut[0];  // std::max_element (:221)
+  for (int k = 1; k < lut_len; ++k)
+    if (a.cmax < lut[k]) a.cmax = lut[k];
+  a.slope_lo = slopes[0];
+  a.slope_hi = slopes[n_slopes - 1];
+  a.n_slopes = n_slopes;
+  a.n_locs = n_locs;
+  a.lut_len = lut_len;
+  a.lut = c->d_lut;
+  a.elevation = elevation;
+  a.terrain_map = terrain_map;
+  a.st = cost_state(st);
+  a.F = dF;
+  HIPC(c, dymu::launch_cost_map(a, s));
+  return DYMU_OK;
+}
+
+int dymu_pack_speed(dymu_ctx* c, uint32_t nx, uint32_t ny, uint64_t ld, double global_res,
+                    const dymu_cost_state* st, double* dF, void* stream) {
+  if (!c || !cost_state_ok(st) || !dF || nx == 0 || ny == 0 || ld < nx) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  dymu::CostArgs a{};
+  a.nx = nx;
+  a.ny = ny;
+  a.ld = (int64_t)ld;
+  a.res = global_res;
+  a.st = cost_state(st);
+  a.F = dF;
+  HIPC(c, dymu::launch_pack_speed(a, pick_stream(c, stream)));
   return DYMU_OK;
 }
 

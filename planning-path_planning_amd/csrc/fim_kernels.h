@@ -81,6 +81,31 @@ hipError_t launch_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,
 hipError_t launch_eikonal_batch(const double* tx, const double* ty, const double* c, double* out,
                                 uint64_t n, int fast, hipStream_t st);
 hipError_t launch_sum_counts(const uint32_t* counts, int32_t* out, hipStream_t st);
+// computeCostMap state (SoA planner node fields, row-major pitch ld)
+struct CostState {
+  double* cost;
+  double* raw_cost;
+  double* slope;
+  uint32_t* terrain;
+  uint8_t* is_obstacle;
+  double* hazard;
+  double* traff;
+  int32_t* loc_mode;
+};
+struct CostArgs {
+  uint32_t nx, ny;
+  int64_t ld;
+  double res, cmax, slope_lo, slope_hi;
+  int n_slopes, n_locs, lut_len;
+  const double* lut;  // device copy
+  const double* elevation;
+  const double* terrain_map;
+  CostState st;
+  double* F;  // speed output (may be null for launch_cost_map)
+};
+hipError_t launch_cost_map(const CostArgs& a, hipStream_t st);
+hipError_t launch_pack_speed(const CostArgs& a, hipStream_t st);
+
 hipError_t launch_prio_init(const double* F, int64_t ld, int64_t nx, int64_t ny,
                            unsigned long long* keys, uint64_t nkeys, uint32_t* hist, uint64_t nhist,
                            unsigned long long* minkey, double* base, double* delta, double kappa,

@@ -63,6 +63,13 @@ class DymuDomain(ctypes.Structure):
     ]
 
 
+class DymuCostState(ctypes.Structure):
+    """dymu_cost_state: device pointers of the planner node fields."""
+    FIELDS = ("cost", "raw_cost", "slope", "terrain", "is_obstacle", "hazard", "traff",
+              "loc_mode")
+    _fields_ = [(f, ctypes.c_void_p) for f in FIELDS]
+
+
 class DymuStats(ctypes.Structure):
     _fields_ = [
         ("passes", ctypes.c_uint64),
@@ -108,6 +115,11 @@ FIM_SYMBOLS = {
     "dymu_dom_finish": (_i32, [_vp, _vp, ctypes.POINTER(DymuStats)]),
     "dymu_last_pass_timing": (_i32, [_vp, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_uint64)]),
+    "dymu_compute_cost_map": (_i32, [_vp, _u32, _u32, _u64, ctypes.c_double, _dp, _i32, _dp,
+                                     _i32, _i32, _vp, _vp, ctypes.POINTER(DymuCostState), _vp,
+                                     _vp]),
+    "dymu_pack_speed": (_i32, [_vp, _u32, _u32, _u64, ctypes.c_double,
+                               ctypes.POINTER(DymuCostState), _vp, _vp]),
     "dymu_strerror": (ctypes.c_char_p, [_i32]),
     "dymu_last_error": (ctypes.c_char_p, [_vp]),
     "dymu_abi_version": (_i32, []),
@@ -269,6 +281,27 @@ class Engine:
         finally:
             for p in ptrs:
                 self.free(p)
+
+    # ---- computeCostMap on the device ----
+    @staticmethod
+    def cost_state(ptrs: dict) -> DymuCostState:
+        """ptrs: field name -> device pointer (int), see DymuCostState.FIELDS."""
+        return DymuCostState(*[ptrs[f] for f in DymuCostState.FIELDS])
+
+    def compute_cost_map(self, nx, ny, ld, res, lut, slopes, n_locs, d_elev, d_terrain,
+                         state: dict, dF=0, stream=0):
+        lut = np.ascontiguousarray(lut, dtype=np.float64)
+        slopes = np.ascontiguousarray(slopes, dtype=np.float64)
+        st = self.cost_state(state)
+        _check(self._lib.dymu_compute_cost_map(self.ctx, nx, ny, ld, res, lut, len(lut), slopes,
+                                               len(slopes), n_locs, d_elev, d_terrain,
+                                               ctypes.byref(st), dF or None, stream or None),
+               self.ctx)
+
+    def pack_speed(self, nx, ny, ld, res, state: dict, dF, stream=0):
+        st = self.cost_state(state)
+        _check(self._lib.dymu_pack_speed(self.ctx, nx, ny, ld, res, ctypes.byref(st), dF,
+                                         stream or None), self.ctx)
 
     def set_profiling(self, period):
         """Time every `period`-th pass launch (True = every launch, 0/False = off)."""

@@ -20,7 +20,7 @@ n = len(disp["FETCH_SIZE"])
 fetch = tot["FETCH_SIZE"] * 1024.0
 write = tot["WRITE_SIZE"] * 1024.0
 out = {
-    "kernel": name, "dispatches": n,
+    "kernel": name, "dispatches": n, "grid": int(sys.argv[4]) if len(sys.argv) > 4 else 16384,
     "fetch_bytes_raw": fetch, "write_bytes": write,
     "traffic_bytes_per_launch": (2.0 * fetch + write) / max(n, 1),
     "traffic_bytes_per_launch_raw": (fetch + write) / max(n, 1),
