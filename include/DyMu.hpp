@@ -89,6 +89,9 @@ class DyMuPathPlanner {
   unsigned goalI() const { return goal_i_; }
   unsigned goalJ() const { return goal_j_; }
   const dymu_stats& lastStats() const { return stats_; }
+  // How the last computeTotalCostMap / computeEntireTotalCostMap ran: 0 cold
+  // solve, 1 windowed re-propagation from the changed speed window, 2 map reused.
+  int lastSolveKind() const { return incremental_; }
   // Local-layer feedback on the global layer (the writes of
   // src/DyMu_LocalPathRepairing.cpp:264-274 and :389-394), row-major ny*nx.
   bool setHazardDensity(const std::vector<double>& hd);
@@ -125,7 +128,11 @@ class DyMuPathPlanner {
   dymu_ctx* ctx_ = nullptr;
   dymu_opts opts_{-1, 0, 0, 0, 0, 0, 0};
   dymu_stats stats_{};
-  std::vector<double> speed_;  // packed F
+  std::vector<double> speed_;   // F of the last solve
+  std::vector<double> packed_;  // F being packed
+  bool solved_ = false;         // the engine holds T of speed_ for the goal below
+  unsigned solved_gi_ = 0, solved_gj_ = 0;
+  int incremental_ = 0;  // last solve: 0 cold, 1 windowed re-propagation, 2 reused
 };
 
 }  // namespace PathPlanning_lib

@@ -153,6 +153,28 @@ int dymu_device_free(dymu_ctx* ctx, void* dptr);
 int dymu_memcpy_d2h(dymu_ctx* ctx, void* dst, const void* src, size_t bytes);
 int dymu_memcpy_h2d(dymu_ctx* ctx, void* dst, const void* src, size_t bytes);
 
+/* ---- dynamic update: windowed re-propagation ----
+ * After the speed changed only inside the window [i0, i0+w) x [j0, j0+h)
+ * (the local layer's hazard / trafficability writes, reference
+ * src/DyMu_LocalPathRepairing.cpp:264-274, :389-394, entering F through
+ * src/DyMu_GlobalPathPlanning.cpp:527-528), bring T from the converged map of
+ * the old speed to that of the new one without a cold solve: cells whose old
+ * T is below theta = min(old T over the window and its 1-cell ring) provably
+ * keep their value; the rest is reset and re-propagated from the boundary of
+ * the kept region.  Increases and decreases are both handled;
+ * the result is the fixed point a cold dymu_solve of the new speed reaches.
+ * The window is clipped to the grid. */
+int dymu_resolve_window_device(dymu_ctx* ctx, const double* dF, double* dT, uint32_t nx,
+                               uint32_t ny, uint64_t ld, uint32_t goal_i, uint32_t goal_j,
+                               uint32_t i0, uint32_t j0, uint32_t w, uint32_t h, void* stream,
+                               dymu_stats* stats);
+/* Host-buffer form: requires that the previous dymu_solve / dymu_resolve_window
+ * on this context solved the same grid size and goal (DYMU_ERR_STATE otherwise);
+ * only the window of F is uploaded, the whole new T is written to T_out. */
+int dymu_resolve_window(dymu_ctx* ctx, const double* F, uint32_t nx, uint32_t ny, uint32_t goal_i,
+                        uint32_t goal_j, uint32_t i0, uint32_t j0, uint32_t w, uint32_t h,
+                        double* T_out, dymu_stats* stats);
+
 /* ---- computeCostMap on the device ----
  * Planner node state (the globalNode fields of reference src/DyMu.hpp:69-108
  * that the global layer uses) as device SoA arrays, row-major, pitch ld. */

@@ -68,6 +68,9 @@ int dymu_planner_set_hazard_density(dymu_planner* p, const double* hd);
 int dymu_planner_set_trafficability(dymu_planner* p, const double* tr);
 /* statistics of the last solve */
 int dymu_planner_last_stats(dymu_planner* p, dymu_stats* out);
+/* how the last solve ran: 0 cold, 1 windowed re-propagation from the window
+ * where the speed changed (dymu_resolve_window), 2 previous map reused */
+int dymu_planner_last_solve_kind(dymu_planner* p);
 
 #ifdef __cplusplus
 }

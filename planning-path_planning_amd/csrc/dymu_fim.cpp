@@ -57,6 +57,7 @@ struct dymu_ctx {
   unsigned long long* d_prio = nullptr;
   uint32_t epoch_base = 0;
   uint32_t* h_count = nullptr;  // pinned
+  unsigned long long* d_scratch = nullptr;  // 8 words of per-call device scalars
   double* d_lut = nullptr;      // computeCostMap LUT (device copy)
   size_t lut_cap = 0;
 
@@ -64,6 +65,9 @@ struct dymu_ctx {
   double* d_F = nullptr;
   double* d_T = nullptr;
   uint64_t cells_cap = 0;
+  // the staged d_T holds the converged map of the last host solve of this grid
+  bool host_valid = false;
+  uint32_t host_nx = 0, host_ny = 0, host_gi = 0, host_gj = 0;
 
   // current domain (whole grid or one row slab) being solved
   struct Dom {
@@ -137,6 +141,7 @@ int ensure_prio(dymu_ctx* c, uint32_t ntiles) {
 
 int ensure_cells(dymu_ctx* c, uint64_t cells) {
   if (cells <= c->cells_cap) return DYMU_OK;
+  c->host_valid = false;
   if (c->d_F) (void)hipFree(c->d_F);
   if (c->d_T) (void)hipFree(c->d_T);
   c->d_F = c->d_T = nullptr;
@@ -160,8 +165,11 @@ int tile_h(int variant) { return variant == 1 ? kTileH : variant == 5 ? 16 : kWa
 bool is_prio(int variant) { return variant == 4 || variant == 5; }
 
 // ---- domain primitives (whole grid, or one row slab with ghost rows) ----
+// cold = true: T := +inf (incl. ghost rows) and the goal seeded (a fresh solve);
+// false: T is kept and the caller seeds list 0 (windowed re-propagation).
 int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t nrows, uint64_t ld,
-              int ghost_lo, int ghost_hi, int64_t gi, int64_t gj, hipStream_t st) {
+              int ghost_lo, int ghost_hi, int64_t gi, int64_t gj, hipStream_t st,
+              bool cold = true) {
   if (!dF || !dT || nx == 0 || nrows == 0 || ld < nx) return DYMU_ERR_ARG;
   int variant = c->variant;
   if (variant == 0) {
@@ -196,7 +204,8 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   }
   HIPC(c, hipMemsetAsync(c->d_counts, 0, sizeof(uint32_t) * 3 * kShards, st));
   HIPC(c, hipMemsetAsync(c->d_stats, 0, sizeof(unsigned long long) * kShards * kStatSlots, st));
-  HIPC(c, launch_fill_inf(dT, ld, nx, ghost_lo ? -1 : 0, (int64_t)nrows + (ghost_hi ? 1 : 0), st));
+  if (cold)
+    HIPC(c, launch_fill_inf(dT, ld, nx, ghost_lo ? -1 : 0, (int64_t)nrows + (ghost_hi ? 1 : 0), st));
   PassArgs& a = D.a;
   if (is_prio(D.variant)) {
     HIPC(c, launch_prio_init(dF, (int64_t)ld, nx, nrows, c->d_keys, 3ull * ntiles, c->d_hist,
@@ -210,7 +219,7 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
     a.target_frac = c->prio_frac;
     a.delta = prio_delta(c);
   }
-  if (gj >= 0) {
+  if (cold && gj >= 0) {
     const uint32_t gtile = (uint32_t)(gj / THd) * ntx + (uint32_t)(gi / TWd);
     HIPC(c, launch_seed(dT, ld, gi, gj, D.lists[0], D.counts[0], c->d_tile_epoch, D.eb + 1, gtile,
                         1, st));
@@ -400,15 +409,12 @@ int dom_finish(dymu_ctx* c, hipStream_t st, dymu_stats* stats, double ms) {
   return DYMU_OK;
 }
 
-int solve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
-               uint32_t gi, uint32_t gj, hipStream_t st, dymu_stats* stats) {
-  if (gi >= nx || gj >= ny) return DYMU_ERR_ARG;
-  int rc = dom_begin(c, dF, dT, nx, ny, ld, 0, 0, gi, gj, st);
-  if (rc) return rc;
+// passes until no tile is queued, then statistics (the domain must be live)
+int converge(dymu_ctx* c, hipStream_t st, dymu_stats* stats) {
   HIPC(c, hipEventRecord(c->ev0, st));
   uint64_t K = c->opts.passes_per_check > 0 ? (uint64_t)c->opts.passes_per_check : 4;
   for (;;) {
-    rc = dom_launch(c, K, st);
+    int rc = dom_launch(c, K, st);
     if (rc) return rc;
     uint64_t pending = 0;
     rc = dom_pending(c, st, &pending);
@@ -427,6 +433,57 @@ int solve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t 
   float ms = 0.f;
   HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
   return dom_finish(c, st, stats, ms);
+}
+
+int solve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
+               uint32_t gi, uint32_t gj, hipStream_t st, dymu_stats* stats) {
+  if (gi >= nx || gj >= ny) return DYMU_ERR_ARG;
+  int rc = dom_begin(c, dF, dT, nx, ny, ld, 0, 0, gi, gj, st);
+  if (rc) return rc;
+  return converge(c, st, stats);
+}
+
+// Windowed re-propagation (update_kernels.hip): dT holds the converged map of
+// the previous speed, dF the new speed, which differs only inside the window.
+int resolve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
+                 uint32_t gi, uint32_t gj, uint32_t i0, uint32_t j0, uint32_t w, uint32_t h,
+                 hipStream_t st, dymu_stats* stats) {
+  if (gi >= nx || gj >= ny || w == 0 || h == 0 || i0 >= nx || j0 >= ny) return DYMU_ERR_ARG;
+  int rc = dom_begin(c, dF, dT, nx, ny, ld, 0, 0, -1, -1, st, /*cold=*/false);
+  if (rc) return rc;
+  auto& D = c->dom;
+  // theta = min old T over the window plus its 1-cell ring (clipped)
+  const uint32_t wi0 = i0 > 0 ? i0 - 1 : 0, wj0 = j0 > 0 ? j0 - 1 : 0;
+  const uint32_t wi1 = (uint32_t)std::min<uint64_t>((uint64_t)i0 + w + 1, nx);
+  const uint32_t wj1 = (uint32_t)std::min<uint64_t>((uint64_t)j0 + h + 1, ny);
+  unsigned long long* theta = c->d_scratch;
+  const unsigned long long inf_bits = 0x7FF0000000000000ull;
+  HIPC(c, hipMemcpyAsync(theta, &inf_bits, sizeof inf_bits, hipMemcpyHostToDevice, st));
+  HIPC(c, launch_window_min(dT, (int64_t)ld, wi0, wj0, wi1, wj1, theta, st));
+  UpdateArgs u{};
+  u.T = dT;
+  u.F = dF;
+  u.ld = (int64_t)ld;
+  u.nx = nx;
+  u.ny = ny;
+  u.gi = gi;
+  u.gj = gj;
+  u.theta_bits = theta;
+  u.list = D.lists[0];
+  u.counts = D.counts[0];
+  u.shard_cap = D.ntiles;
+  u.tile_epoch = c->d_tile_epoch;
+  u.epoch = D.eb + 1;  // the epoch of list 0 (dom_launch: eb + p + 2 for list p + 1)
+  u.tw = (uint32_t)tile_w(D.variant);
+  u.th = (uint32_t)tile_h(D.variant);
+  u.ntx = (uint32_t)D.a.ntx;
+  if (is_prio(D.variant)) {
+    u.keys = prio_keys(c, 0);
+    u.hist = prio_hist(c, 0);
+    HIPC(c, launch_theta_state(theta, prio_minkey(c, 0), prio_base(c, 0), st));
+  }
+  HIPC(c, launch_reset_seed(u, st));
+  return converge(c, st, stats);
 }
 
 hipStream_t pick_stream(dymu_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
@@ -507,6 +564,7 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
     if (const char* kv = std::getenv("DYMU_PRIO_DEBUG")) c->prio_debug = std::atoi(kv);
   }
   if (e == hipSuccess) e = hipMalloc(&c->d_counts, sizeof(uint32_t) * 4 * kShards);
+  if (e == hipSuccess) e = hipMalloc(&c->d_scratch, sizeof(unsigned long long) * 8);
   if (e == hipSuccess)
     e = hipMalloc(&c->d_stats, sizeof(unsigned long long) * kShards * kStatSlots);
   if (e == hipSuccess) e = hipHostMalloc(&c->h_count, sizeof(uint32_t) * 4 * kShards, hipHostMallocDefault);
@@ -533,6 +591,7 @@ int dymu_destroy(dymu_ctx* c) {
   if (c->d_prio) (void)hipFree(c->d_prio);
   if (c->d_trace) (void)hipFree(c->d_trace);
   if (c->d_lut) (void)hipFree(c->d_lut);
+  if (c->d_scratch) (void)hipFree(c->d_scratch);
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->d_F) (void)hipFree(c->d_F);
   if (c->d_T) (void)hipFree(c->d_T);
@@ -556,11 +615,55 @@ int dymu_solve(dymu_ctx* c, const double* F, uint32_t nx, uint32_t ny, uint32_t 
   const uint64_t cells = (uint64_t)nx * ny;
   int rc = ensure_cells(c, cells);
   if (rc) return rc;
+  c->host_valid = false;
   HIPC(c, hipMemcpyAsync(c->d_F, F, sizeof(double) * cells, hipMemcpyHostToDevice, c->stream));
   rc = solve_core(c, c->d_F, c->d_T, nx, ny, nx, gi, gj, c->stream, stats);
   if (rc) return rc;
   HIPC(c, hipMemcpyAsync(T_out, c->d_T, sizeof(double) * cells, hipMemcpyDeviceToHost, c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
+  c->host_valid = true;
+  c->host_nx = nx;
+  c->host_ny = ny;
+  c->host_gi = gi;
+  c->host_gj = gj;
+  return DYMU_OK;
+}
+
+int dymu_resolve_window_device(dymu_ctx* c, const double* dF, double* dT, uint32_t nx,
+                               uint32_t ny, uint64_t ld, uint32_t gi, uint32_t gj, uint32_t i0,
+                               uint32_t j0, uint32_t w, uint32_t h, void* stream,
+                               dymu_stats* stats) {
+  if (!c || !dF || !dT || nx == 0 || ny == 0 || ld < nx) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  w = (uint32_t)std::min<uint64_t>(w, nx > i0 ? nx - i0 : 0);
+  h = (uint32_t)std::min<uint64_t>(h, ny > j0 ? ny - j0 : 0);
+  return resolve_core(c, dF, dT, nx, ny, ld, gi, gj, i0, j0, w, h, pick_stream(c, stream), stats);
+}
+
+int dymu_resolve_window(dymu_ctx* c, const double* F, uint32_t nx, uint32_t ny, uint32_t gi,
+                        uint32_t gj, uint32_t i0, uint32_t j0, uint32_t w, uint32_t h,
+                        double* T_out, dymu_stats* stats) {
+  if (!c || !F || !T_out || nx == 0 || ny == 0) return DYMU_ERR_ARG;
+  if (!c->host_valid || c->host_nx != nx || c->host_ny != ny || c->host_gi != gi ||
+      c->host_gj != gj) {
+    c->last_error = "dymu_resolve_window: no previous dymu_solve of this grid and goal";
+    return DYMU_ERR_STATE;
+  }
+  if (i0 >= nx || j0 >= ny || w == 0 || h == 0) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  w = (uint32_t)std::min<uint64_t>(w, nx - i0);
+  h = (uint32_t)std::min<uint64_t>(h, ny - j0);
+  c->host_valid = false;
+  // only the window of F changed: upload those rows' columns
+  const uint64_t off = (uint64_t)j0 * nx + i0;
+  HIPC(c, hipMemcpy2DAsync(c->d_F + off, sizeof(double) * nx, F + off, sizeof(double) * nx,
+                           sizeof(double) * w, h, hipMemcpyHostToDevice, c->stream));
+  int rc = resolve_core(c, c->d_F, c->d_T, nx, ny, nx, gi, gj, i0, j0, w, h, c->stream, stats);
+  if (rc) return rc;
+  const uint64_t cells = (uint64_t)nx * ny;
+  HIPC(c, hipMemcpyAsync(T_out, c->d_T, sizeof(double) * cells, hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  c->host_valid = true;
   return DYMU_OK;
 }
 
@@ -684,7 +787,7 @@ int dymu_compute_cost_map(dymu_ctx* c, uint32_t nx, uint32_t ny, uint64_t ld, do
   HIPC(c, hipSetDevice(c->device));
   hipStream_t s = pick_stream(c, stream);
   if ((size_t)lut_len > c->lut_cap) {
-    if (c->d_lut) (void)hipFree(c->d_lut);
+    if (c->d_lut) HIPC(c, hipFree(c->d_lut));
     c->d_lut = nullptr;
     c->lut_cap = 0;
     HIPC(c, hipMalloc(&c->d_lut, sizeof(double) * (size_t)lut_len));

@@ -106,6 +106,28 @@ struct CostArgs {
 hipError_t launch_cost_map(const CostArgs& a, hipStream_t st);
 hipError_t launch_pack_speed(const CostArgs& a, hipStream_t st);
 
+// windowed re-propagation (update_kernels.hip)
+struct UpdateArgs {
+  double* T;
+  const double* F;
+  int64_t ld;
+  uint32_t nx, ny, gi, gj;
+  const unsigned long long* theta_bits;
+  uint32_t* list;    // list 0 (kShards x shard_cap)
+  uint32_t* counts;  // its kShards counters
+  uint32_t shard_cap;
+  uint32_t* tile_epoch;
+  uint32_t epoch;
+  uint32_t tw, th, ntx;
+  unsigned long long* keys;  // priority kernels: keys / histogram of list 0, else null
+  uint32_t* hist;
+};
+hipError_t launch_window_min(const double* T, int64_t ld, uint32_t i0, uint32_t j0, uint32_t i1,
+                             uint32_t j1, unsigned long long* out, hipStream_t st);
+hipError_t launch_reset_seed(const UpdateArgs& a, hipStream_t st);
+hipError_t launch_theta_state(const unsigned long long* theta_bits, unsigned long long* minkey0,
+                              double* base0, hipStream_t st);
+
 hipError_t launch_prio_init(const double* F, int64_t ld, int64_t nx, int64_t ny,
                            unsigned long long* keys, uint64_t nkeys, uint32_t* hist, uint64_t nhist,
                            unsigned long long* minkey, double* base, double* delta, double kappa,

@@ -6,6 +6,7 @@
 // reference's does); the total-cost propagation -- the reference's FMM loop
 // -- is one dymu_solve() call on the GPU.
 #include <algorithm>
+#include <cstring>
 #include <cmath>
 #include <cstdio>
 #include <limits>
@@ -50,6 +51,7 @@ bool DyMuPathPlanner::initGlobalLayer(double globalres, double localres, unsigne
                                       unsigned num_nodes_Y, std::vector<double> offset) {
   global_res_ = globalres;
   local_res_ = localres;
+  solved_ = false;
   nx_ = num_nodes_X;
   ny_ = num_nodes_Y;
   global_offset_ = offset;
@@ -229,11 +231,16 @@ bool DyMuPathPlanner::setTrafficability(const std::vector<double>& tr) {
 
 // The engine call: F = global_res * cost * (2 + hazard - traff) (:527-528),
 // +inf for obstacles; T and node states come back for every cell.
+// Incremental path: when the previous solve on this engine was
+// of the same grid and goal and the speed changed only inside a window (the
+// local layer's hazard / trafficability writes), the engine re-propagates
+// from that window (dymu_resolve_window) instead of solving cold; unchanged
+// speed reuses the previous map.  Both give the cold solve's fixed point.
 bool DyMuPathPlanner::solveFull() {
   const uint64_t n = (uint64_t)nx_ * ny_;
-  speed_.resize(n);
+  packed_.resize(n);
   for (uint64_t k = 0; k < n; ++k)
-    speed_[k] = is_obstacle_[k] ? kInf : global_res_ * cost_[k] * (2 + hazard_[k] - traff_[k]);
+    packed_[k] = is_obstacle_[k] ? kInf : global_res_ * cost_[k] * (2 + hazard_[k] - traff_[k]);
   if (!ctx_) {
     const int rc = dymu_create(&ctx_, &opts_);
     if (rc != DYMU_OK) {
@@ -241,12 +248,46 @@ bool DyMuPathPlanner::solveFull() {
       throw std::runtime_error(std::string("dymu: cannot create the HIP engine: ") +
                                dymu_strerror(rc));
     }
+    solved_ = false;
   }
-  const int rc = dymu_solve(ctx_, speed_.data(), nx_, ny_, goal_i_, goal_j_, total_cost_.data(),
-                            &stats_);
-  if (rc != DYMU_OK)
-    throw std::runtime_error(std::string("dymu_solve failed: ") + dymu_strerror(rc) + " " +
-                             dymu_last_error(ctx_));
+  int rc = DYMU_ERR_STATE;
+  if (solved_ && speed_.size() == n && solved_gi_ == goal_i_ && solved_gj_ == goal_j_) {
+    // bounding box of the cells whose speed changed (bitwise)
+    unsigned i0 = nx_, i1 = 0, j0 = ny_, j1 = 0;
+    for (unsigned j = 0; j < ny_; ++j) {
+      const double* a = &packed_[idx(0, j)];
+      const double* b = &speed_[idx(0, j)];
+      if (std::memcmp(a, b, sizeof(double) * nx_) == 0) continue;
+      for (unsigned i = 0; i < nx_; ++i)
+        if (std::memcmp(a + i, b + i, sizeof(double)) != 0) {
+          i0 = std::min(i0, i);
+          i1 = std::max(i1, i + 1);
+        }
+      j0 = std::min(j0, j);
+      j1 = j + 1;
+    }
+    if (i1 == 0) {  // nothing changed: the map stands
+      incremental_ = 2;
+      return true;
+    }
+    if ((uint64_t)(i1 - i0) * (j1 - j0) * 4 <= n) {  // a window: re-propagate from it
+      rc = dymu_resolve_window(ctx_, packed_.data(), nx_, ny_, goal_i_, goal_j_, i0, j0, i1 - i0,
+                               j1 - j0, total_cost_.data(), &stats_);
+      if (rc == DYMU_OK) incremental_ = 1;
+    }
+  }
+  if (rc != DYMU_OK) {
+    solved_ = false;
+    rc = dymu_solve(ctx_, packed_.data(), nx_, ny_, goal_i_, goal_j_, total_cost_.data(), &stats_);
+    if (rc != DYMU_OK)
+      throw std::runtime_error(std::string("dymu_solve failed: ") + dymu_strerror(rc) + " " +
+                               dymu_last_error(ctx_));
+    incremental_ = 0;
+  }
+  speed_.swap(packed_);
+  solved_ = true;
+  solved_gi_ = goal_i_;
+  solved_gj_ = goal_j_;
   for (uint64_t k = 0; k < n; ++k) state_[k] = total_cost_[k] < kInf ? CLOSED : OPEN;
   return true;
 }

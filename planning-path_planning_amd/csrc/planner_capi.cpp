@@ -203,4 +203,9 @@ int dymu_planner_last_stats(dymu_planner* p, dymu_stats* out) {
   return DYMU_OK;
 }
 
+int dymu_planner_last_solve_kind(dymu_planner* p) {
+  if (!p) return DYMU_ERR_ARG;
+  return p->pl.lastSolveKind();
+}
+
 }  // extern "C"

@@ -1,0 +1,128 @@
+// update_kernels.hip -- windowed re-propagation after a local speed change
+// (the hazard bumps of reference
+// src/DyMu_LocalPathRepairing.cpp:264-274 and trafficability drops :389-394
+// change F = res*cost*(2+hd-tr) (src/DyMu_GlobalPathPlanning.cpp:527-528)
+// inside a window W).
+//
+// Causality of the update (:531-535): a cell's converged value exceeds every
+// neighbour value it was computed from (one-sided: min + C; two-sided:
+// >= max(Tx, Ty) because |Tx-Ty| < C).  Let theta = min of the old T over W and
+// its 1-cell ring.  A cell whose old T < theta depends on no cell of W, and no
+// path through W can give it a smaller value (such a path leaves the ring at a
+// value >= theta), so it keeps its value exactly.  Every other cell may change:
+// reset it to +inf, seed the tiles where a reset cell touches a kept finite
+// cell, and run the FIM.  New values of reset cells are >= theta, so theta is
+// a valid priority key for the seeded tiles.  The result is the fixed point of
+// a cold solve.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fim_kernels.h"
+
+namespace dymu {
+
+namespace {
+
+constexpr unsigned long long kInfBits = 0x7FF0000000000000ull;
+
+__device__ __forceinline__ unsigned long long dbits(double v) {
+  return (unsigned long long)__double_as_longlong(v);
+}
+
+// theta = min T over [i0,i1) x [j0,j1) (window plus ring, clipped); T >= 0 so
+// the u64 bit patterns order like the doubles.
+__global__ void k_window_min(const double* T, int64_t ld, uint32_t i0, uint32_t j0, uint32_t i1,
+                             uint32_t j1, unsigned long long* out) {
+  __shared__ unsigned long long s_min;
+  if (threadIdx.x == 0) s_min = kInfBits;
+  __syncthreads();
+  const uint64_t w = i1 - i0, n = w * (uint64_t)(j1 - j0);
+  unsigned long long m = kInfBits;
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const double v = T[(int64_t)(j0 + c / w) * ld + (i0 + c % w)];
+    const unsigned long long b = dbits(v);
+    m = b < m ? b : m;
+  }
+  atomicMin(&s_min, m);
+  __syncthreads();
+  if (threadIdx.x == 0 && s_min != kInfBits) atomicMin(out, s_min);
+}
+
+// Reset every cell with old T >= theta (except the goal) and seed the tiles
+// holding a reset, finite-speed cell next to a kept finite cell.  A neighbour
+// read may race with its reset, but "old < theta" cells are never written, so
+// the test below sees the same answer either way.
+__global__ void k_reset_seed(UpdateArgs a) {
+  const double theta = __longlong_as_double((long long)*a.theta_bits);
+  const uint64_t n = (uint64_t)a.nx * a.ny;
+  const uint32_t shard = blockIdx.x % kShards;
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t j = (uint32_t)(c / a.nx), i = (uint32_t)(c % a.nx);
+    const int64_t k = (int64_t)j * a.ld + i;
+    if (i == a.gi && j == a.gj) continue;
+    const double old = a.T[k];
+    if (!(old >= theta)) continue;  // kept
+    if (old < __builtin_inf()) a.T[k] = __builtin_inf();
+    if (!(a.F[k] < __builtin_inf())) continue;  // obstacle: never updated
+    // kept neighbour: old T < theta, or the goal (theta = 0 when the goal is in
+    // the window or its ring)
+    auto kept = [&](uint32_t ii, uint32_t jj, int64_t kk) {
+      return a.T[kk] < theta || (ii == a.gi && jj == a.gj);
+    };
+    bool seed = false;
+    if (j > 0) seed |= kept(i, j - 1, k - a.ld);
+    if (i > 0) seed |= kept(i - 1, j, k - 1);
+    if (i + 1 < a.nx) seed |= kept(i + 1, j, k + 1);
+    if (j + 1 < a.ny) seed |= kept(i, j + 1, k + a.ld);
+    if (!seed) continue;
+    const uint32_t tile = (j / a.th) * a.ntx + (i / a.tw);
+    if (atomicMax(&a.tile_epoch[tile], a.epoch) < a.epoch) {
+      const uint32_t pos = atomicAdd(&a.counts[shard], 1u);
+      a.list[(uint64_t)shard * a.shard_cap + pos] = tile;
+      if (a.keys) {  // priority kernels: key theta, histogram bin 0
+        atomicMin(&a.keys[tile], *a.theta_bits);
+        atomicAdd(&a.hist[shard * kBins], 1u);
+      }
+    }
+  }
+}
+
+// Priority-kernel list-0 state: keys of the seeded tiles are theta.
+__global__ void k_theta_state(const unsigned long long* theta_bits, unsigned long long* minkey0,
+                              double* base0) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    *minkey0 = *theta_bits;
+    const double th = __longlong_as_double((long long)*theta_bits);
+    *base0 = th < __builtin_inf() ? th : 0.0;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_window_min(const double* T, int64_t ld, uint32_t i0, uint32_t j0, uint32_t i1,
+                             uint32_t j1, unsigned long long* out, hipStream_t st) {
+  const uint64_t n = (uint64_t)(i1 - i0) * (j1 - j0);
+  uint64_t b = (n + 255) / 256;
+  if (b > 1024) b = 1024;
+  if (b == 0) b = 1;
+  hipLaunchKernelGGL(k_window_min, dim3((unsigned)b), dim3(256), 0, st, T, ld, i0, j0, i1, j1, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_reset_seed(const UpdateArgs& a, hipStream_t st) {
+  uint64_t b = ((uint64_t)a.nx * a.ny + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b == 0) b = 1;
+  hipLaunchKernelGGL(k_reset_seed, dim3((unsigned)b), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_theta_state(const unsigned long long* theta_bits, unsigned long long* minkey0,
+                              double* base0, hipStream_t st) {
+  hipLaunchKernelGGL(k_theta_state, dim3(1), dim3(64), 0, st, theta_bits, minkey0, base0);
+  return hipGetLastError();
+}
+
+}  // namespace dymu

@@ -120,6 +120,10 @@ FIM_SYMBOLS = {
                                      _vp]),
     "dymu_pack_speed": (_i32, [_vp, _u32, _u32, _u64, ctypes.c_double,
                                ctypes.POINTER(DymuCostState), _vp, _vp]),
+    "dymu_resolve_window_device": (_i32, [_vp, _vp, _vp, _u32, _u32, _u64, _u32, _u32, _u32,
+                                          _u32, _u32, _u32, _vp, ctypes.POINTER(DymuStats)]),
+    "dymu_resolve_window": (_i32, [_vp, _dp, _u32, _u32, _u32, _u32, _u32, _u32, _u32, _u32,
+                                   _dp, ctypes.POINTER(DymuStats)]),
     "dymu_strerror": (ctypes.c_char_p, [_i32]),
     "dymu_last_error": (ctypes.c_char_p, [_vp]),
     "dymu_abi_version": (_i32, []),
@@ -208,6 +212,27 @@ class Engine:
         _check(self._lib.dymu_solve(self.ctx, F, nx, ny, goal_i, goal_j, T, ctypes.byref(st)),
                self.ctx)
         return SolveResult(T, st.as_dict())
+
+    def resolve_window(self, F: np.ndarray, goal_i: int, goal_j: int, i0: int, j0: int, w: int,
+                       h: int) -> SolveResult:
+        """Windowed re-propagation after F changed inside [i0,i0+w) x [j0,j0+h);
+        the previous solve on this engine must be of the same grid and goal."""
+        F = np.ascontiguousarray(F, dtype=np.float64)
+        ny, nx = F.shape
+        T = np.empty_like(F)
+        st = DymuStats()
+        _check(self._lib.dymu_resolve_window(self.ctx, F, nx, ny, goal_i, goal_j, i0, j0, w, h, T,
+                                             ctypes.byref(st)), self.ctx)
+        return SolveResult(T, st.as_dict())
+
+    def resolve_window_device(self, dF: int, dT: int, nx: int, ny: int, ld: int, goal_i: int,
+                              goal_j: int, i0: int, j0: int, w: int, h: int,
+                              stream: int = 0) -> dict:
+        st = DymuStats()
+        _check(self._lib.dymu_resolve_window_device(self.ctx, dF, dT, nx, ny, ld, goal_i, goal_j,
+                                                    i0, j0, w, h, stream or None,
+                                                    ctypes.byref(st)), self.ctx)
+        return st.as_dict()
 
     # -- device-resident solve --
     def solve_device(self, dF: int, dT: int, nx: int, ny: int, ld: int, goal_i: int,
@@ -351,6 +376,7 @@ PLANNER_SYMBOLS = {
     "dymu_planner_set_hazard_density": (_i32, [_vp, _dp]),
     "dymu_planner_set_trafficability": (_i32, [_vp, _dp]),
     "dymu_planner_last_stats": (_i32, [_vp, ctypes.POINTER(DymuStats)]),
+    "dymu_planner_last_solve_kind": (_i32, [_vp]),
 }
 
 _pl = None
@@ -370,6 +396,12 @@ def load_planner() -> ctypes.CDLL:
             fn.argtypes = args
         _pl = lib
     return _pl
+
+
+def _b_int(rc: int) -> int:
+    if rc < 0:
+        raise DymuError(rc)
+    return rc
 
 
 def _b(rc: int) -> bool:
@@ -491,6 +523,10 @@ class Planner:
 
     def setTrafficability(self, tr) -> bool:
         return _b(self._lib.dymu_planner_set_trafficability(self.h, self._grid(tr)))
+
+    def lastSolveKind(self) -> int:
+        """0 cold solve, 1 windowed re-propagation, 2 previous map reused."""
+        return _b_int(self._lib.dymu_planner_last_solve_kind(self.h))
 
     def lastStats(self) -> dict:
         st = DymuStats()

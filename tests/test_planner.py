@@ -185,3 +185,43 @@ def test_dynamic_hazard_feedback(dymu, oracle):
     T = p.totalCostRaw()
     fin = np.isfinite(Tref)
     assert (np.abs(T[fin] - Tref[fin]) / np.maximum(1, Tref[fin])).max() <= RTOL
+
+
+@pytest.mark.gpu
+def test_incremental_resolve_through_planner(dymu, oracle):
+    """Config 5 through the class surface: a hazard bump on a disc (the local
+    layer's write, LocalPathRepairing.cpp:264-274) followed by
+    computeTotalCostMap re-propagates from the changed window only
+    (lastSolveKind 1) and equals the cold solve / oracle; an unchanged speed
+    reuses the map (2); a goal change solves cold (0)."""
+    N = 200
+    F = oracle.synth_speed(N, N, seed=12, obst_frac=0.02, obst_seed=13, goal=(150, 150))
+    F[158:163, 38:43] = 2.0  # room for the second goal
+    p = dymu.Planner()
+    p.initGlobalLayer(1.0, 0.5, N, N)
+    p.setCostMap(np.where(np.isfinite(F), F, -1.0))
+    assert p.setGoal((150, 150))
+    assert p.computeEntireTotalCostMap() and p.lastSolveKind() == 0
+    cold_visits = p.lastStats()["tile_visits"]
+    assert p.computeEntireTotalCostMap() and p.lastSolveKind() == 2
+    hd = p.getHazardDensityMatrix()
+    j, i = np.mgrid[0:N, 0:N]
+    inner = (i - 60) ** 2 + (j - 50) ** 2 <= 15 ** 2
+    ring = ((i - 60) ** 2 + (j - 50) ** 2 <= 16 ** 2) & ~inner
+    hd[inner] = np.minimum(1.0, hd[inner] + 1.0)
+    hd[ring] = np.minimum(1.0, hd[ring] + 0.1)
+    assert p.setHazardDensity(hd)
+    p.computeEntireTotalCostMap()
+    assert p.lastSolveKind() == 1
+    assert p.lastStats()["tile_visits"] < cold_visits
+    obst = ~np.isfinite(F)
+    Fr = oracle.pack_speed(np.where(obst, -1.0, F), hd, p.getTrafficabilityMatrix(), obst,
+                           res=1.0)
+    Tref, _ = oracle.fmm(Fr, (150, 150))
+    T = p.totalCostRaw()
+    assert np.array_equal(np.isinf(T), np.isinf(Tref))
+    fin = np.isfinite(Tref)
+    assert (np.abs(T[fin] - Tref[fin]) / np.maximum(1, Tref[fin])).max() <= RTOL
+    assert p.setGoal((40, 160))
+    p.computeEntireTotalCostMap()
+    assert p.lastSolveKind() == 0
