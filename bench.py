@@ -46,7 +46,7 @@ def parse():
                     help="no per-launch events (roofline reported as null)")
     ap.add_argument("--backend", default="nccl",
                     help="N>1 only: 'nccl' (RCCL over xGMI) or 'gloo' (host-staged rehearsal)")
-    ap.add_argument("--passes-per-exchange", type=int, default=4)
+    ap.add_argument("--passes-per-exchange", type=int, default=16)
     return ap.parse_args()
 
 

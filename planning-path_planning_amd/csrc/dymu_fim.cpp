@@ -41,6 +41,8 @@ struct dymu_ctx {
   float prio_frac = 0.0f;    // v4: ... or this fraction of the active list (DYMU_PRIO_FRAC)
   int prio_trace = -1;       // v4: stamp phases of this pass index (DYMU_PRIO_TRACE)
   unsigned long long* d_trace = nullptr;
+  int prune = 1;             // v4/v5 exact activation pruning (DYMU_PRUNE=0 disables)
+  int occupancy[6] = {0, 8, 8, 6, 5, 4};  // pass workgroups per CU (occupancy API)
   int prio_debug = 0;        // v4: print the state after the first N passes (DYMU_PRIO_DEBUG)
 
   // tile workspace
@@ -217,6 +219,7 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
     a.target = c->prio_target ? c->prio_target
                               : (uint32_t)c->cu_count * (D.variant == 5 ? 8u : 64u);
     a.target_frac = c->prio_frac;
+    a.prune = c->prune;
     a.delta = prio_delta(c);
   }
   if (cold && gj >= 0) {
@@ -241,9 +244,9 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   a.shard_cap = ntiles;
   a.tile_epoch = c->d_tile_epoch;
   a.stats = c->d_stats;
-  // resident workgroups per CU at the kernels' register budgets (v3: 76 VGPRs -> 6 waves/SIMD)
+  // resident workgroups per CU at the kernel's register / LDS budget
   D.blocks = c->opts.grid_blocks > 0 ? c->opts.grid_blocks
-                                      : c->cu_count * (D.variant == 5 ? 4 : D.variant == 4 ? 5 : D.variant == 3 ? 6 : 8);
+                                      : c->cu_count * c->occupancy[D.variant];
   D.live = true;
   return DYMU_OK;
 }
@@ -540,6 +543,8 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
       c->cu_count = prop.multiProcessorCount;
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   }
+  if (e == hipSuccess)
+    for (int v = 1; v <= 5; ++v) c->occupancy[v] = pass_blocks_per_cu(v);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (c->opts.kernel < 0 || c->opts.kernel > 5 || c->opts.prio_target < 0) {
@@ -561,6 +566,7 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
       c->prio_min_tiles = (uint32_t)std::atol(kv);
     if (const char* kv = std::getenv("DYMU_PRIO_FRAC")) c->prio_frac = (float)std::atof(kv);
     if (const char* kv = std::getenv("DYMU_PRIO_TRACE")) c->prio_trace = std::atoi(kv);
+    if (const char* kv = std::getenv("DYMU_PRUNE")) c->prune = std::atoi(kv);
     if (const char* kv = std::getenv("DYMU_PRIO_DEBUG")) c->prio_debug = std::atoi(kv);
   }
   if (e == hipSuccess) e = hipMalloc(&c->d_counts, sizeof(uint32_t) * 4 * kShards);

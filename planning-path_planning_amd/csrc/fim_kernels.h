@@ -51,11 +51,14 @@ struct PassArgs {
   const double* delta;    // histogram bin width (k_prio_init)
   uint32_t target;        // tiles to relax per pass; 0 = all (plain FIM)
   float target_frac;      // ... at least this fraction of the active list
+  int prune;              // activate a neighbour only through edge cells below its halo value
   unsigned long long* trace;  // debug: kTracePts s_memrealtime stamps per block, or null
 };
 
-constexpr int kBins = 64;
-constexpr int kTracePts = 10;  // v4 key histogram bins
+constexpr int kBins = 64;  // v4/v5 key histogram bins
+constexpr int kTracePts = 10;
+// resident 256-thread workgroups per CU of a pass kernel variant (occupancy API)
+int pass_blocks_per_cu(int variant);
 
 hipError_t launch_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, int64_t row_hi,
                            hipStream_t st);

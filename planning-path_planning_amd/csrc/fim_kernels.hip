@@ -788,13 +788,34 @@ __device__ __forceinline__ int visit8(const PassArgs& a, double* img, unsigned l
   if (db) a.T[gj * a.ld + gib] = tb;
   const unsigned long long vr = dr ? dbits(tr) : kInfBits;
   const unsigned long long vb = db ? dbits(tb) : kInfBits;
-  const unsigned long long vrb = vr < vb ? vr : vb;
-  if (r == 0 && vrb != kInfBits) atomicMin(&ek[0], vrb);
-  if (r == WT - 1 && vrb != kInfBits) atomicMin(&ek[3], vrb);
-  const unsigned long long vw = cr == 0 ? vr : (cb == 0 ? vb : kInfBits);
-  const unsigned long long ve = cr == WT - 1 ? vr : (cb == WT - 1 ? vb : kInfBits);
-  if (vw != kInfBits) atomicMin(&ek[1], vw);
-  if (ve != kInfBits) atomicMin(&ek[2], ve);
+  // An edge cell n can only improve the cell x across the edge if its new value
+  // is below x's (every candidate of x's update using n is >= T(n), :531-535);
+  // x's halo snapshot is >= its current value, so the test is safe (prune).
+  // The halo ring of the image is never written by the sweeps: it is re-read
+  // there rather than kept live in registers.
+  auto across = [&](unsigned long long v, double hx) {
+    return (v != kInfBits && (!a.prune || v < dbits(hx))) ? v : kInfBits;
+  };
+  const int odd = r & 1;
+  if (r == 0) {  // cr = 2q, cb = 2q+1
+    const unsigned long long m0 = across(vr, img[1 + 2 * q]), m1 = across(vb, img[2 + 2 * q]);
+    const unsigned long long m = m0 < m1 ? m0 : m1;
+    if (m != kInfBits) atomicMin(&ek[0], m);
+  }
+  if (r == WT - 1) {  // cr = 2q+1, cb = 2q
+    const unsigned long long m0 = across(vb, img[(WT + 1) * IP + 1 + 2 * q]);
+    const unsigned long long m1 = across(vr, img[(WT + 1) * IP + 2 + 2 * q]);
+    const unsigned long long m = m0 < m1 ? m0 : m1;
+    if (m != kInfBits) atomicMin(&ek[3], m);
+  }
+  if (q == 0) {  // column 0: red on even rows, black on odd rows
+    const unsigned long long m = across(odd ? vb : vr, img[(r + 1) * IP]);
+    if (m != kInfBits) atomicMin(&ek[1], m);
+  }
+  if (q == 3) {  // column 7: red on odd rows, black on even rows
+    const unsigned long long m = across(odd ? vr : vb, img[(r + 1) * IP + WT + 1]);
+    if (m != kInfBits) atomicMin(&ek[2], m);
+  }
   return sweeps;
 }
 
@@ -910,13 +931,35 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
     v[cr[k] - 4 * q] = dr ? dbits(tr[k]) : kInfBits;
     v[cb[k] - 4 * q] = db ? dbits(tb[k]) : kInfBits;
   }
-  const unsigned long long m01 = v[0] < v[1] ? v[0] : v[1];
-  const unsigned long long m23 = v[2] < v[3] ? v[2] : v[3];
-  const unsigned long long vall = m01 < m23 ? m01 : m23;
-  if (r == 0 && vall != kInfBits) atomicMin(&ek[0], vall);
-  if (r == TT - 1 && vall != kInfBits) atomicMin(&ek[3], vall);
-  if (q == 0 && v[0] != kInfBits) atomicMin(&ek[1], v[0]);
-  if (q == 3 && v[3] != kInfBits) atomicMin(&ek[2], v[3]);
+  // prune as in visit8, halo re-read from the image
+  auto across = [&](unsigned long long vv, double hx) {
+    return (vv != kInfBits && (!a.prune || vv < dbits(hx))) ? vv : kInfBits;
+  };
+  auto min4 = [&](const double* h) {
+    unsigned long long m = kInfBits;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned long long x = across(v[k], h[k]);
+      m = x < m ? x : m;
+    }
+    return m;
+  };
+  if (r == 0) {
+    const unsigned long long m = min4(img + 1 + 4 * q);
+    if (m != kInfBits) atomicMin(&ek[0], m);
+  }
+  if (r == TT - 1) {
+    const unsigned long long m = min4(img + (TT + 1) * IP16 + 1 + 4 * q);
+    if (m != kInfBits) atomicMin(&ek[3], m);
+  }
+  if (q == 0) {
+    const unsigned long long m = across(v[0], img[row]);
+    if (m != kInfBits) atomicMin(&ek[1], m);
+  }
+  if (q == 3) {
+    const unsigned long long m = across(v[3], img[row + TT + 1]);
+    if (m != kInfBits) atomicMin(&ek[2], m);
+  }
   return sweeps;
 }
 
@@ -1328,6 +1371,25 @@ hipError_t launch_pass_prio16(const PassArgs& a, int blocks, hipStream_t st, hip
   else
     hipLaunchKernelGGL(k_fim_pass_prio<16>, dim3(blocks), dim3(256), 0, st, a);
   return hipGetLastError();
+}
+
+int pass_blocks_per_cu(int variant) {
+  int n = 0;
+  hipError_t e = hipErrorInvalidValue;
+  switch (variant) {
+    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass, 256, 0); break;
+    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_w8, 256, 0); break;
+    case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_rb, 256, 0); break;
+    case 4:
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_prio<8>, 256, 0);
+      break;
+    case 5:
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_prio<16>, 256, 0);
+      break;
+    default: break;
+  }
+  (void)hipGetLastError();
+  return (e == hipSuccess && n > 0) ? n : 4;
 }
 
 hipError_t launch_prio_init(const double* F, int64_t ld, int64_t nx, int64_t ny,

@@ -196,3 +196,25 @@ def test_sampled_pass_timing(dymu, oracle):
             eng.set_profiling(-1)
     finally:
         eng.close()
+
+
+def serpentine_maze(F, period=64, offset=32):
+    """SURVEY s8(d) config-3 stress variant: 1-cell walls every `period` rows,
+    each with one gap, alternating between the left and the right end."""
+    F = F.copy()
+    ny, nx = F.shape
+    for k, j in enumerate(range(offset, ny, period)):
+        F[j, :] = np.inf
+        F[j, 1 if k % 2 == 0 else nx - 2] = 2.0
+    return F
+
+
+@pytest.mark.parametrize("N,period", [(256, 16), (384, 32)])
+def test_parity_serpentine_maze(kengine, oracle, N, period):
+    g = (N // 2, N // 2 + 4)
+    F = serpentine_maze(oracle.synth_speed(N, N, seed=9, obst_frac=0.01, obst_seed=2, goal=g),
+                        period, period // 2)
+    r = kengine.solve(F, *g)
+    Tref, _ = oracle.fmm(F, g)
+    assert_parity(r.T, Tref)
+    assert r.stats["passes"] > 4 * N // (r.stats["tile_w"] * 2)  # the maze inflates the passes
