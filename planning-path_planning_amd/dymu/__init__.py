@@ -19,7 +19,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIBDIR = os.path.normpath(os.path.join(_HERE, "..", "lib"))
+# DYMU_LIBDIR: load the libraries from another directory (A/B builds)
+_LIBDIR = os.environ.get("DYMU_LIBDIR") or os.path.normpath(os.path.join(_HERE, "..", "lib"))
 
 DYMU_OK = 0
 _ERRS = {
