@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--backend", default="nccl",
                     help="N>1 only: 'nccl' (RCCL over xGMI) or 'gloo' (host-staged rehearsal)")
     ap.add_argument("--passes-per-exchange", type=int, default=16)
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the row-slab path even at N=1 (exercises the RCCL code path)")
     return ap.parse_args()
 
 
@@ -115,7 +117,7 @@ def main():
     args = parse()
     world = args.gpus
     rank = int(os.environ.get("RANK", "0"))
-    if world > 1:
+    if world > 1 or args.sharded:
         import torch  # noqa: F401  (before dymu: one HIP runtime in the process)
         import bench_sharded
 
@@ -135,10 +137,12 @@ def main():
         launch_s = kern_ms * 1e-3 / kern_n  # mean duration of a pass launch (sampled events)
         # (i) SURVEY s8(d)(i), the judged figure: 16 B per cell per solve (read F + write T
         # once), spread over the solve's pass launches
-        bytes_i = N * N * BYTES_PER_CELL_SOLVE * K / tot["launches"]
+        cells = tot.get("slab_cells", N * N)  # N>1: rank 0's slab, rank 0's launches
+        bytes_i = cells * BYTES_PER_CELL_SOLVE * K / tot["launches"]
         achieved = bytes_i / launch_s / 1e9
         # (ii) diagnostic sweep efficiency: 24 B per cell-visit in the launch
-        cells_visited = tot["tile_visits"] * st["tile_w"] * st["tile_h"]
+        visits = tot.get("rank0_tile_visits", tot["tile_visits"])
+        cells_visited = visits * st["tile_w"] * st["tile_h"]
         bytes_ii = cells_visited * BYTES_PER_CELL_VISIT / tot["launches"]
         roof = {
             "bound": "hbm",

@@ -11,6 +11,8 @@ import torch.distributed as dist
 import dymu
 from dymu.sharded import SlabSolver
 
+PROFILE_PERIOD = 8  # time every 8th pass launch of rank 0 (bench.py's roofline)
+
 
 def run(args):
     rank = int(os.environ.get("RANK", "0"))
@@ -37,6 +39,9 @@ def run(args):
                         passes_per_exchange=args.passes_per_exchange, check_every=4)
     for _ in range(args.warmup):
         solver.solve(F, T_buf, g[0], g[1])
+    prof = not args.no_profile
+    eng.set_profiling(PROFILE_PERIOD if prof else 0)
+    kern_ms, kern_n = 0.0, 0
     tot = {"passes": 0, "tile_visits": 0, "inner_sweeps": 0, "launches": 0, "rounds": 0}
     dist.barrier()
     torch.cuda.synchronize()
@@ -45,18 +50,25 @@ def run(args):
         st = solver.solve(F, T_buf, g[0], g[1])
         for k in tot:
             tot[k] += st[k]
+        if prof:
+            ms, nl = eng.last_pass_timing()
+            kern_ms += ms
+            kern_n += nl
     torch.cuda.synchronize()
     dist.barrier()
     dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
                       device=device if backend == "nccl" else "cpu")
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    tot["rank0_tile_visits"] = tot["tile_visits"]  # this rank's (rank 0 reports)
     agg = torch.tensor([tot["tile_visits"], tot["inner_sweeps"], tot["passes"]],
                        dtype=torch.float64, device=dt.device)
     dist.all_reduce(agg)
     tot["tile_visits"], tot["inner_sweeps"] = int(agg[0]), int(agg[1])
     tot["passes_sum_ranks"] = int(agg[2])
+    tot["slab_cells"] = nrows * N  # rank 0's slab: the roofline's per-launch bytes
+    eng.set_profiling(0)
     eng.close()
     dist.destroy_process_group()
     if rank != 0:
         return None
-    return float(dt.item()), tot, 0.0, 0, st
+    return float(dt.item()), tot, kern_ms, kern_n, st

@@ -42,13 +42,7 @@ struct dymu_ctx {
   int prio_trace = -1;       // v4: stamp phases of this pass index (DYMU_PRIO_TRACE)
   unsigned long long* d_trace = nullptr;
   int prune = 1;             // v4/v5 exact activation pruning (DYMU_PRUNE=0 disables)
-  int occupancy[9] = {0, 8, 8, 6, 5, 4, 8, 5, 4};  // pass workgroups per CU (occupancy API)
-  int strided = 0;  // DYMU_STRIDED=1: strided classify shares (A/B)
-  int split = 0;  // v4/v5 passes as classify + visit launches (DYMU_SPLIT=1; slower today)
-  uint32_t* d_ready = nullptr;  // split passes: dense ready list + keys, 2 counters
-  unsigned long long* d_ready_key = nullptr;
-  uint32_t* d_ready_cnt = nullptr;
-  uint32_t ready_cap = 0;
+  int occupancy[6] = {0, 8, 8, 6, 5, 4};  // pass workgroups per CU (occupancy API)
   int prio_debug = 0;        // v4: print the state after the first N passes (DYMU_PRIO_DEBUG)
 
   // tile workspace
@@ -147,20 +141,6 @@ int ensure_prio(dymu_ctx* c, uint32_t ntiles) {
   return DYMU_OK;
 }
 
-int ensure_ready(dymu_ctx* c, uint32_t ntiles) {
-  if (!c->d_ready_cnt) HIPC(c, hipMalloc(&c->d_ready_cnt, sizeof(uint32_t) * 2));
-  if (ntiles <= c->ready_cap) return DYMU_OK;
-  if (c->d_ready) (void)hipFree(c->d_ready);
-  if (c->d_ready_key) (void)hipFree(c->d_ready_key);
-  c->d_ready = nullptr;
-  c->d_ready_key = nullptr;
-  c->ready_cap = 0;
-  HIPC(c, hipMalloc(&c->d_ready, sizeof(uint32_t) * (uint64_t)ntiles));
-  HIPC(c, hipMalloc(&c->d_ready_key, sizeof(unsigned long long) * (uint64_t)ntiles));
-  c->ready_cap = ntiles;
-  return DYMU_OK;
-}
-
 int ensure_cells(dymu_ctx* c, uint64_t cells) {
   if (cells <= c->cells_cap) return DYMU_OK;
   c->host_valid = false;
@@ -209,7 +189,6 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   int rc = ensure_tiles(c, ntiles);
   if (rc) return rc;
   if (is_prio(variant) && (rc = ensure_prio(c, ntiles)) != DYMU_OK) return rc;
-  if (is_prio(variant) && c->split && (rc = ensure_ready(c, ntiles)) != DYMU_OK) return rc;
   auto& D = c->dom;
   D = dymu_ctx::Dom{};
   D.variant = variant;
@@ -241,12 +220,6 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
                               : (uint32_t)c->cu_count * (D.variant == 5 ? 8u : 64u);
     a.target_frac = c->prio_frac;
     a.prune = c->prune;
-    a.strided = c->strided;
-    if (c->split) {
-      HIPC(c, hipMemsetAsync(c->d_ready_cnt, 0, sizeof(uint32_t) * 2, st));
-      a.ready = c->d_ready;
-      a.ready_key = c->d_ready_key;
-    }
     a.delta = prio_delta(c);
   }
   if (cold && gj >= 0) {
@@ -302,8 +275,6 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
       a.minkey_clear = prio_minkey(c, (p + 2) % 3);
       a.base_in = prio_base(c, p % 3);
       a.base_out = prio_base(c, (p + 1) % 3);
-      a.ready_count = c->d_ready_cnt + (p & 1);
-      a.ready_count_next = c->d_ready_cnt + ((p + 1) & 1);
     }
     const bool tr = is_prio(D.variant) && c->prio_trace >= 0 && p == (uint64_t)c->prio_trace;
     if (tr) {
@@ -325,10 +296,6 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
     }
     HIPC(c, D.variant == 1   ? launch_pass(a, D.blocks, st, e0, e1)
             : D.variant == 2 ? launch_pass_w8(a, D.blocks, st, e0, e1)
-            : (is_prio(D.variant) && a.ready)
-                ? launch_prio_split(a, tile_w(D.variant), c->cu_count * c->occupancy[6],
-                                    c->cu_count * c->occupancy[D.variant == 5 ? 8 : 7], st, e0,
-                                    e1)
             : D.variant == 4 ? launch_pass_prio(a, D.blocks, st, e0, e1)
             : D.variant == 5 ? launch_pass_prio16(a, D.blocks, st, e0, e1)
                               : launch_pass_rb(a, D.blocks, st, e0, e1));
@@ -577,7 +544,7 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   }
   if (e == hipSuccess)
-    for (int v = 1; v <= 8; ++v) c->occupancy[v] = pass_blocks_per_cu(v);
+    for (int v = 1; v <= 5; ++v) c->occupancy[v] = pass_blocks_per_cu(v);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (c->opts.kernel < 0 || c->opts.kernel > 5 || c->opts.prio_target < 0) {
@@ -600,8 +567,6 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
     if (const char* kv = std::getenv("DYMU_PRIO_FRAC")) c->prio_frac = (float)std::atof(kv);
     if (const char* kv = std::getenv("DYMU_PRIO_TRACE")) c->prio_trace = std::atoi(kv);
     if (const char* kv = std::getenv("DYMU_PRUNE")) c->prune = std::atoi(kv);
-    if (const char* kv = std::getenv("DYMU_SPLIT")) c->split = std::atoi(kv);
-    if (const char* kv = std::getenv("DYMU_STRIDED")) c->strided = std::atoi(kv);
     if (const char* kv = std::getenv("DYMU_PRIO_DEBUG")) c->prio_debug = std::atoi(kv);
   }
   if (e == hipSuccess) e = hipMalloc(&c->d_counts, sizeof(uint32_t) * 4 * kShards);
@@ -633,9 +598,6 @@ int dymu_destroy(dymu_ctx* c) {
   if (c->d_trace) (void)hipFree(c->d_trace);
   if (c->d_lut) (void)hipFree(c->d_lut);
   if (c->d_scratch) (void)hipFree(c->d_scratch);
-  if (c->d_ready) (void)hipFree(c->d_ready);
-  if (c->d_ready_key) (void)hipFree(c->d_ready_key);
-  if (c->d_ready_cnt) (void)hipFree(c->d_ready_cnt);
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->d_F) (void)hipFree(c->d_F);
   if (c->d_T) (void)hipFree(c->d_T);

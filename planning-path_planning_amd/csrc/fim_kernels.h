@@ -51,23 +51,14 @@ struct PassArgs {
   const double* delta;    // histogram bin width (k_prio_init)
   uint32_t target;        // tiles to relax per pass; 0 = all (plain FIM)
   float target_frac;      // ... at least this fraction of the active list
-  int strided;            // v4/v5: workgroup b classifies entries b, b+G, ... (else a chunk)
   int prune;              // activate a neighbour only through edge cells below its halo value
-  // split passes (k_prio_classify + k_prio_visit): dense ready list of the pass
-  uint32_t* ready;
-  unsigned long long* ready_key;
-  uint32_t* ready_count;       // this pass (appended by the classify kernel)
-  uint32_t* ready_count_next;  // the next pass's (cleared by classify block 0)
   unsigned long long* trace;  // debug: kTracePts s_memrealtime stamps per block, or null
 };
 
 constexpr int kBins = 64;  // v4/v5 key histogram bins
 constexpr int kTracePts = 10;
 // resident 256-thread workgroups per CU of a pass kernel variant (occupancy API)
-// (6: k_prio_classify, 7: k_prio_visit<8>, 8: k_prio_visit<16>)
 int pass_blocks_per_cu(int variant);
-hipError_t launch_prio_split(const PassArgs& a, int tile, int blocks_classify, int blocks_visit,
-                             hipStream_t st, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 
 hipError_t launch_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, int64_t row_hi,
                            hipStream_t st);

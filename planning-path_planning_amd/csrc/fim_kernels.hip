@@ -1100,20 +1100,16 @@ __global__ __launch_bounds__(256, 4) void k_fim_pass_prio(PassArgs a) {
   const unsigned long long hmask =
       TS == 16 ? ~0ull : (half ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull);
 
-  // this workgroup's share of the active list: a contiguous chunk, or (strided)
-  // every gridDim-th entry -- ready tiles cluster in list order (they were
-  // appended by neighbouring tiles), striding spreads them over the workgroups
-  const uint32_t G = gridDim.x, b = blockIdx.x;
-  const uint32_t chunk = (n_active + G - 1) / G;
-  const uint32_t c0 = a.strided ? 0u : b * chunk;
-  const uint32_t c1 = a.strided ? (n_active > b ? (n_active - b + G - 1) / G : 0u)
-                                : min(n_active, c0 + chunk);
+  // this workgroup's share of the active list: a contiguous chunk
+  const uint32_t chunk = (n_active + gridDim.x - 1) / gridDim.x;
+  const uint32_t c0 = blockIdx.x * chunk;
+  const uint32_t c1 = min(n_active, c0 + chunk);
   for (uint32_t s0 = c0; s0 < c1; s0 += WCAP) {  // block-uniform
     const uint32_t s1 = min(c1, s0 + WCAP);
     if (tid == 0) s_nwork = 0;
     __syncthreads();
     for (uint32_t e = s0 + tid; e < s1; e += blockDim.x) {
-      const uint32_t t = list_at(a.list_in, a.shard_cap, s_pref, a.strided ? b + e * G : e);
+      const uint32_t t = list_at(a.list_in, a.shard_cap, s_pref, e);
       const unsigned long long kb = a.key_in[t];
       a.key_in[t] = kInfBits;
       if (key_bin(bitsd(kb), origin_in, inv_delta) <= bstar) {
@@ -1207,246 +1203,6 @@ __global__ __launch_bounds__(256, 4) void k_fim_pass_prio(PassArgs a) {
     trace[4] = __builtin_amdgcn_s_memrealtime();
     trace[5] = ((unsigned long long)(c1 > c0 ? c1 - c0 : 0) << 32) | (unsigned long long)s_visits;
   }
-}
-
-// ---------------------------------------------------------------------------
-// Split priority pass: the single-kernel pass above gives each
-// workgroup a contiguous chunk of the active list and relaxes the ready tiles
-// of that chunk itself, so a workgroup with more ready tiles than wave slots
-// runs a second round while others idle.  Here a pass is two launches:
-//   k_prio_classify  scan + classify every active tile: ready ones are
-//                    compacted into one dense list (one atomic per chunk),
-//                    deferred ones re-appended to list p+1;
-//   k_prio_visit<TS> every wave takes ready tiles by global index, so the
-//                    ready tiles spread evenly over all waves of the chip.
-// ---------------------------------------------------------------------------
-struct EnqLds {
-  uint32_t* q;
-  uint32_t* nq;
-  uint32_t* hout;
-  unsigned long long* minout;
-};
-
-// append tile t with key kb to list p+1 (key = running min over activations)
-__device__ __forceinline__ void prio_enqueue(const PassArgs& a, const EnqLds& L, uint32_t shard,
-                                             double origin_out, double inv_delta, uint32_t t,
-                                             unsigned long long kb) {
-  atomicMin(&a.key_out[t], kb);
-  atomicMin(L.minout, kb);
-  if (atomicMax(&a.tile_epoch[t], a.epoch) < a.epoch) {
-    atomicAdd(&L.hout[key_bin(bitsd(kb), origin_out, inv_delta)], 1u);
-    const uint32_t pos = atomicAdd(L.nq, 1u);
-    if (pos < QCAP) {
-      L.q[pos] = t;
-    } else {
-      const uint32_t gp = atomicAdd(&a.count_out[shard], 1u);
-      a.list_out[(uint64_t)shard * a.shard_cap + gp] = t;
-    }
-  }
-}
-
-// publish the workgroup's LDS queue, histogram and min key (after a barrier)
-__device__ __forceinline__ void prio_flush(const PassArgs& a, const EnqLds& L, uint32_t shard,
-                                           uint32_t* s_base, int tid) {
-  const uint32_t nq = *L.nq < QCAP ? *L.nq : QCAP;
-  if (tid == 0) {
-    if (nq) *s_base = atomicAdd(&a.count_out[shard], nq);
-    if (*L.minout != kInfBits) atomicMin(a.minkey_out, *L.minout);
-  }
-  if (tid < kBins && L.hout[tid]) atomicAdd(&a.hist_out[shard * kBins + tid], L.hout[tid]);
-  __syncthreads();
-  for (uint32_t k = tid; k < nq; k += blockDim.x)
-    a.list_out[(uint64_t)shard * a.shard_cap + *s_base + k] = L.q[k];
-}
-
-__global__ __launch_bounds__(256) void k_prio_classify(PassArgs a) {
-  __shared__ uint32_t s_q[QCAP];
-  __shared__ uint32_t s_rt[WCAP];
-  __shared__ unsigned long long s_rk[WCAP];
-  __shared__ uint32_t s_pref[kShards + 1];
-  __shared__ uint32_t s_hout[kBins];
-  __shared__ uint32_t s_nq, s_base, s_nr, s_rbase;
-  __shared__ int s_bstar;
-  __shared__ unsigned long long s_minout;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wv = tid >> 6;
-  const uint32_t shard = blockIdx.x % kShards;
-  const double delta = *a.delta;
-  const double origin_in = *a.base_in;
-  const double origin_out = bitsd(*a.minkey_in);
-  const double inv_delta = 1.0 / delta;
-  if (wv == 0) {
-    uint32_t c = lane < kShards ? a.count_in[lane] : 0u;
-    uint32_t h = 0;
-#pragma unroll
-    for (int k = 0; k < kShards; ++k) h += a.hist_in[k * kBins + lane];
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t yc = __shfl_up(c, o), yh = __shfl_up(h, o);
-      if (lane >= o) {
-        c += yc;
-        h += yh;
-      }
-    }
-    if (lane < kShards) s_pref[lane + 1] = c;
-    const uint32_t n = __shfl(c, kShards - 1);
-    const uint32_t fr = (uint32_t)(a.target_frac * (float)n);
-    const uint32_t target = a.target > fr ? a.target : fr;
-    const unsigned long long m = __ballot(h >= target && lane < kBins - 1);
-    if (lane == 0) {
-      s_pref[0] = 0u;
-      s_bstar = (a.target > 0 && n > target && m) ? (int)__ffsll((long long)m) - 1 : kBins;
-      s_nq = 0;
-      s_minout = kInfBits;
-    }
-  }
-  s_hout[tid & (kBins - 1)] = 0u;
-  __syncthreads();
-  const uint32_t n_active = s_pref[kShards];
-  const int bstar = s_bstar;
-  if (blockIdx.x == 0) {
-    if (tid < kShards) a.count_clear[tid] = 0u;
-    if (tid == 0) *a.ready_count_next = 0u;
-    for (int k = tid; k < kShards * kBins; k += blockDim.x) a.hist_clear[k] = 0u;
-    if (tid == 0) {
-      *a.minkey_clear = kInfBits;
-      *a.base_out = origin_out;
-      if (n_active > 0) {
-        atomicAdd(&a.stats[kStatPasses], 1ull);
-        atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
-      }
-    }
-  }
-  const EnqLds L{s_q, &s_nq, s_hout, &s_minout};
-  const uint32_t chunk = (n_active + gridDim.x - 1) / gridDim.x;
-  const uint32_t c0 = blockIdx.x * chunk;
-  const uint32_t c1 = min(n_active, c0 + chunk);
-  for (uint32_t s0 = c0; s0 < c1; s0 += WCAP) {  // block-uniform
-    const uint32_t s1 = min(c1, s0 + WCAP);
-    if (tid == 0) s_nr = 0;
-    __syncthreads();
-    for (uint32_t e = s0 + tid; e < s1; e += blockDim.x) {
-      const uint32_t t = list_at(a.list_in, a.shard_cap, s_pref, e);
-      const unsigned long long kb = a.key_in[t];
-      a.key_in[t] = kInfBits;
-      if (key_bin(bitsd(kb), origin_in, inv_delta) <= bstar) {
-        const uint32_t pos = atomicAdd(&s_nr, 1u);
-        s_rt[pos] = t;
-        s_rk[pos] = kb;
-      } else {
-        prio_enqueue(a, L, shard, origin_out, inv_delta, t, kb);  // deferred
-      }
-    }
-    __syncthreads();
-    const uint32_t nr = s_nr;
-    if (tid == 0 && nr) s_rbase = atomicAdd(a.ready_count, nr);
-    __syncthreads();
-    for (uint32_t k = tid; k < nr; k += blockDim.x) {
-      a.ready[s_rbase + k] = s_rt[k];
-      a.ready_key[s_rbase + k] = s_rk[k];
-    }
-    __syncthreads();
-  }
-  prio_flush(a, L, shard, &s_base, tid);
-}
-
-template <int TS>
-__global__ __launch_bounds__(256) void k_prio_visit(PassArgs a) {
-  constexpr int TPW = TS == 8 ? 2 : 1;
-  constexpr int IMG = TS == 8 ? (WT + 2) * IP : (16 + 2) * IP16;
-  __shared__ uint32_t s_q[QCAP];
-  __shared__ uint32_t s_hout[kBins];
-  __shared__ uint32_t s_nq, s_base;
-  __shared__ unsigned long long s_visits, s_sweeps, s_minout;
-  __shared__ unsigned long long s_ek[4 * TPW][4];
-  __shared__ double s_img[4 * TPW][IMG];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wv = tid >> 6;
-  const int half = lane >> 5;
-  const int hl = lane & 31;
-  const int r = hl >> 2, q = hl & 3;
-  const int cr = 2 * q + (r & 1), cb = 2 * q + 1 - (r & 1);
-  const uint32_t shard = blockIdx.x % kShards;
-  const double inv_delta = 1.0 / *a.delta;
-  const double origin_out = bitsd(*a.minkey_in);
-  const uint32_t n_ready = *a.ready_count;
-  if (tid == 0) {
-    s_nq = 0;
-    s_visits = 0;
-    s_sweeps = 0;
-    s_minout = kInfBits;
-  }
-  s_hout[tid & (kBins - 1)] = 0u;
-  __syncthreads();
-  const EnqLds L{s_q, &s_nq, s_hout, &s_minout};
-  const int slot = TS == 8 ? wv * 2 + half : wv;
-  const int sl = TS == 8 ? hl : lane;
-  double* img = s_img[slot];
-  unsigned long long* ek = s_ek[slot];
-  const unsigned long long hmask =
-      TS == 16 ? ~0ull : (half ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull);
-  unsigned long long my_visits = 0, my_sweeps = 0;
-  const uint32_t stride = gridDim.x * 4u * (uint32_t)TPW;
-  for (uint32_t wb = (blockIdx.x * 4u + (uint32_t)wv) * (uint32_t)TPW; wb < n_ready;
-       wb += stride) {  // wave-uniform
-    const uint32_t li = wb + (uint32_t)(TS == 8 ? half : 0);
-    const bool has = li < n_ready;
-    uint32_t tile = 0;
-    int tx = 0, ty = 0;
-    if (has) {
-      tile = a.ready[li];
-      tx = (int)(tile % (uint32_t)a.ntx);
-      ty = (int)(tile / (uint32_t)a.ntx);
-    }
-    if (sl < 4) ek[sl] = kInfBits;
-    bool capped;
-    int sweeps;
-    if constexpr (TS == 8)
-      sweeps = visit8(a, img, ek, has, tx, ty, r, q, cr, cb, capped);
-    else
-      sweeps = visit16(a, img, ek, has, tx, ty, lane, capped);
-    if (has) {
-      my_visits += 1;
-      my_sweeps += (unsigned long long)sweeps;
-    }
-    const unsigned long long mC = __ballot(capped && has) & hmask;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    bool want = false;
-    int nx_t = tx, ny_t = ty;
-    unsigned long long kb = kInfBits;
-    if (has && sl < 4) {
-      kb = ek[sl];
-      if (sl == 0) { want = kb != kInfBits && ty > 0; ny_t = ty - 1; }
-      else if (sl == 1) { want = kb != kInfBits && tx > 0; nx_t = tx - 1; }
-      else if (sl == 2) { want = kb != kInfBits && tx + 1 < a.ntx; nx_t = tx + 1; }
-      else { want = kb != kInfBits && ty + 1 < a.nty; ny_t = ty + 1; }
-    } else if (has && sl == 4 && mC != 0ull) {
-      want = true;
-      kb = a.ready_key[li];
-    }
-    if (want)
-      prio_enqueue(a, L, shard, origin_out, inv_delta,
-                   (uint32_t)ny_t * (uint32_t)a.ntx + (uint32_t)nx_t, kb);
-    __builtin_amdgcn_wave_barrier();
-  }
-  if (lane == 0 && my_visits) {
-    atomicAdd(&s_visits, my_visits);
-    atomicAdd(&s_sweeps, my_sweeps);
-  }
-  if (TS == 8 && lane == 32 && my_visits) {
-    atomicAdd(&s_visits, my_visits);
-    atomicAdd(&s_sweeps, my_sweeps);
-  }
-  __syncthreads();
-  if (tid == 0 && s_visits) {
-    unsigned long long* st = a.stats + (uint64_t)shard * kStatSlots;
-    atomicAdd(&st[kStatVisits], s_visits);
-    atomicAdd(&st[kStatSweeps], s_sweeps);
-  }
-  prio_flush(a, L, shard, &s_base, tid);
 }
 
 // Priority-pass state for a new solve: every key +inf, histograms zero, list-0
@@ -1652,31 +1408,6 @@ hipError_t launch_pass_prio16(const PassArgs& a, int blocks, hipStream_t st, hip
   return hipGetLastError();
 }
 
-hipError_t launch_prio_split(const PassArgs& a, int tile, int blocks_classify, int blocks_visit,
-                             hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-  if (e0)
-    hipExtLaunchKernelGGL(k_prio_classify, dim3(blocks_classify), dim3(256), 0, st, e0, nullptr,
-                          0, a);
-  else
-    hipLaunchKernelGGL(k_prio_classify, dim3(blocks_classify), dim3(256), 0, st, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  if (tile == 16) {
-    if (e1)
-      hipExtLaunchKernelGGL(k_prio_visit<16>, dim3(blocks_visit), dim3(256), 0, st, nullptr, e1,
-                            0, a);
-    else
-      hipLaunchKernelGGL(k_prio_visit<16>, dim3(blocks_visit), dim3(256), 0, st, a);
-  } else {
-    if (e1)
-      hipExtLaunchKernelGGL(k_prio_visit<8>, dim3(blocks_visit), dim3(256), 0, st, nullptr, e1, 0,
-                            a);
-    else
-      hipLaunchKernelGGL(k_prio_visit<8>, dim3(blocks_visit), dim3(256), 0, st, a);
-  }
-  return hipGetLastError();
-}
-
 int pass_blocks_per_cu(int variant) {
   int n = 0;
   hipError_t e = hipErrorInvalidValue;
@@ -1689,13 +1420,6 @@ int pass_blocks_per_cu(int variant) {
       break;
     case 5:
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_prio<16>, 256, 0);
-      break;
-    case 6: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_prio_classify, 256, 0); break;
-    case 7:
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_prio_visit<8>, 256, 0);
-      break;
-    case 8:
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_prio_visit<16>, 256, 0);
       break;
     default: break;
   }
