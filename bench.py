@@ -76,7 +76,8 @@ def cpu_baseline(n_edge, obst):
 
 PROFILE_PERIOD = 8  # time every 8th pass launch with HIP events (sampled mean duration)
 KERNEL_NAMES = {1: "k_fim_pass(", 2: "k_fim_pass_w8", 3: "k_fim_pass_rb", 4: "k_fim_pass_prio<8>",
-                5: "k_fim_pass_prio<16>"}
+                5: "k_fim_pass_dyn<16>" if os.environ.get("DYMU_DYN", "1") != "0"
+                else "k_fim_pass_prio<16"}
 
 
 def run_single(args):

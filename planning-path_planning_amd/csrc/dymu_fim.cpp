@@ -43,6 +43,8 @@ struct dymu_ctx {
   unsigned long long* d_trace = nullptr;
   int prune = 1;             // v4/v5 exact activation pruning (DYMU_PRUNE=0 disables)
   int occupancy[6] = {0, 8, 8, 6, 5, 4};  // pass workgroups per CU (occupancy API)
+  int wpb = 16;  // kernel 5: waves per workgroup (DYMU_WPB: 4, 8, 16)
+  int dyn = 1;   // kernel 5: wave-level dynamic scheduling (DYMU_DYN=0: classify phase)
   int prio_debug = 0;        // v4: print the state after the first N passes (DYMU_PRIO_DEBUG)
 
   // tile workspace
@@ -297,7 +299,7 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
     HIPC(c, D.variant == 1   ? launch_pass(a, D.blocks, st, e0, e1)
             : D.variant == 2 ? launch_pass_w8(a, D.blocks, st, e0, e1)
             : D.variant == 4 ? launch_pass_prio(a, D.blocks, st, e0, e1)
-            : D.variant == 5 ? launch_pass_prio16(a, D.blocks, st, e0, e1)
+            : D.variant == 5 ? launch_pass_prio16(a, D.blocks, st, e0, e1, c->wpb, c->dyn)
                               : launch_pass_rb(a, D.blocks, st, e0, e1));
     ++D.launches;
     if (tr) {
@@ -543,8 +545,13 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
       c->cu_count = prop.multiProcessorCount;
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   }
-  if (e == hipSuccess)
+  if (const char* kv = std::getenv("DYMU_WPB")) c->wpb = std::atoi(kv);
+  if (c->wpb != 4 && c->wpb != 8) c->wpb = 16;
+  if (const char* kv = std::getenv("DYMU_DYN")) c->dyn = std::atoi(kv) != 0;
+  if (e == hipSuccess) {
     for (int v = 1; v <= 5; ++v) c->occupancy[v] = pass_blocks_per_cu(v);
+    c->occupancy[5] = prio16_blocks_per_cu(c->wpb, c->dyn);
+  }
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   if (c->opts.kernel < 0 || c->opts.kernel > 5 || c->opts.prio_target < 0) {

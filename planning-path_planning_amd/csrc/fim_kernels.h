@@ -72,7 +72,9 @@ hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st,
 hipError_t launch_pass_prio(const PassArgs& a, int blocks, hipStream_t st,
                            hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_pass_prio16(const PassArgs& a, int blocks, hipStream_t st,
-                             hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+                             hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int wpb = 16,
+                             int dyn = 0);
+int prio16_blocks_per_cu(int wpb, int dyn);  // occupancy of launch_pass_prio16's workgroups
 hipError_t launch_pass_rb(const PassArgs& a, int blocks, hipStream_t st,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);     // v3: 2 x 8x8 tiles / wave, red-black
 hipError_t launch_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,

@@ -892,8 +892,16 @@ __device__ __forceinline__ int rb_sweeps4(double* img, const int (&sr)[2], const
   return sweeps;
 }
 
+struct NoGate {
+  __device__ bool operator()() const { return true; }
+};
+
+// gate(): wave-uniform, evaluated after the tile's loads are issued (so a key
+// load the gate waits on overlaps them); false = skip the visit, return -1.
+template <class Gate = NoGate>
 __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned long long* ek,
-                                       bool has, int tx, int ty, int lane, bool& capped) {
+                                       bool has, int tx, int ty, int lane, bool& capped,
+                                       Gate gate = Gate()) {
   constexpr int TT = 16;
   const int r = lane >> 2, q = lane & 3, odd = r & 1;
   const int cr[2] = {4 * q + odd, 4 * q + 2 + odd};
@@ -939,6 +947,8 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
       }
     }
   }
+  asm volatile("" ::: "memory");  // the loads above issue before the gate's wait
+  if (!gate()) return -1;
   if (q == 0) img[row] = hw;
   if (q == 3) img[row + TT + 1] = he;
   if (r == 0) {
@@ -997,11 +1007,14 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
   return sweeps;
 }
 
-template <int TS>  // 8: two 8x8 tiles per wave (v3 body); 16: one 16x16 tile per wave
-__global__ __launch_bounds__(256, 4) void k_fim_pass_prio(PassArgs a) {
+// TS 8: two 8x8 tiles per wave (v3 body); 16: one 16x16 tile per wave.
+// WPB waves per workgroup: bigger workgroups pool the ready tiles of bigger
+// chunks, so fewer of them overflow their wave slots into a second round.
+template <int TS, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_prio(PassArgs a) {
   static_assert(TS == 8 || TS == 16, "tile size");
   constexpr int TPW = TS == 8 ? 2 : 1;  // tiles per wave
-  constexpr int SLOTS = 4 * TPW;         // tile slots per workgroup
+  constexpr int SLOTS = WPB * TPW;       // tile slots per workgroup
   constexpr int IMG = TS == 8 ? (WT + 2) * IP : (16 + 2) * IP16;
   __shared__ uint32_t s_q[QCAP];
   __shared__ uint32_t s_work[WCAP];
@@ -1181,6 +1194,181 @@ __global__ __launch_bounds__(256, 4) void k_fim_pass_prio(PassArgs a) {
     atomicAdd(&s_sweeps, my_sweeps);
   }
   if (TS == 8 && lane == 32 && my_visits) {  // each half counted its own tiles
+    atomicAdd(&s_visits, my_visits);
+    atomicAdd(&s_sweeps, my_sweeps);
+  }
+  __syncthreads();
+  const uint32_t nq = s_nq < QCAP ? s_nq : QCAP;
+  if (tid == 0) {
+    if (nq) s_base = atomicAdd(&a.count_out[shard], nq);
+    if (s_minout != kInfBits) atomicMin(a.minkey_out, s_minout);
+    if (s_visits) {
+      unsigned long long* st = a.stats + (uint64_t)shard * kStatSlots;
+      atomicAdd(&st[kStatVisits], s_visits);
+      atomicAdd(&st[kStatSweeps], s_sweeps);
+    }
+  }
+  if (tid < kBins && s_hout[tid]) atomicAdd(&a.hist_out[shard * kBins + tid], s_hout[tid]);
+  __syncthreads();
+  for (uint32_t k = tid; k < nq; k += blockDim.x)
+    a.list_out[(uint64_t)shard * a.shard_cap + s_base + k] = s_q[k];
+  if (trace && tid == 0) {
+    trace[4] = __builtin_amdgcn_s_memrealtime();
+    trace[5] = ((unsigned long long)(c1 > c0 ? c1 - c0 : 0) << 32) | (unsigned long long)s_visits;
+  }
+}
+
+// Kernel 5 with wave-level dynamic scheduling (16x16 tiles): each wave takes
+// the next entry of its workgroup's chunk from an LDS counter, loads the key
+// and the tile together, and either defers the tile (key above the threshold
+// bin) or visits it.  No classify phase and no block-wide barrier between
+// reading the list and the sweeps: a wave that drew a deferred or a quickly
+// converging tile moves on to the next entry while the others still sweep.
+template <int WPB>
+__global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
+  constexpr int IMG = (16 + 2) * IP16;
+  __shared__ uint32_t s_q[QCAP];
+  __shared__ uint32_t s_pref[kShards + 1];
+  __shared__ uint32_t s_hout[kBins];
+  __shared__ uint32_t s_nq, s_base, s_next;
+  __shared__ int s_bstar;
+  __shared__ unsigned long long s_visits, s_sweeps, s_minout;
+  __shared__ unsigned long long s_ek[WPB][4];
+  __shared__ double s_img[WPB][IMG];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const uint32_t shard = blockIdx.x % kShards;
+  unsigned long long* trace = a.trace ? a.trace + (uint64_t)blockIdx.x * kTracePts : nullptr;
+  if (trace && tid == 0) trace[0] = __builtin_amdgcn_s_memrealtime();
+
+  const double delta = *a.delta;
+  const double origin_in = *a.base_in;
+  const double origin_out = bitsd(*a.minkey_in);
+  const double inv_delta = 1.0 / delta;
+  if (wv == 0) {  // shard prefix counts and the threshold bin (as k_fim_pass_prio)
+    uint32_t c = lane < kShards ? a.count_in[lane] : 0u;
+    uint32_t h = 0;
+#pragma unroll
+    for (int k = 0; k < kShards; ++k) h += a.hist_in[k * kBins + lane];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t yc = __shfl_up(c, o), yh = __shfl_up(h, o);
+      if (lane >= o) {
+        c += yc;
+        h += yh;
+      }
+    }
+    if (lane < kShards) s_pref[lane + 1] = c;
+    const uint32_t n = __shfl(c, kShards - 1);
+    const uint32_t fr = (uint32_t)(a.target_frac * (float)n);
+    const uint32_t target = a.target > fr ? a.target : fr;
+    const unsigned long long m = __ballot(h >= target && lane < kBins - 1);
+    if (lane == 0) {
+      s_pref[0] = 0u;
+      s_bstar = (a.target > 0 && n > target && m) ? (int)__ffsll((long long)m) - 1 : kBins;
+      s_nq = 0;
+      s_next = 0;
+      s_visits = 0;
+      s_sweeps = 0;
+      s_minout = kInfBits;
+    }
+  }
+  s_hout[tid & (kBins - 1)] = 0u;
+  __syncthreads();
+  const uint32_t n_active = s_pref[kShards];
+  const int bstar = s_bstar;
+  if (trace && tid == 0) trace[1] = __builtin_amdgcn_s_memrealtime();
+  if (blockIdx.x == 0) {
+    if (tid < kShards) a.count_clear[tid] = 0u;
+    for (int k = tid; k < kShards * kBins; k += blockDim.x) a.hist_clear[k] = 0u;
+    if (tid == 0) {
+      *a.minkey_clear = kInfBits;
+      *a.base_out = origin_out;
+      if (n_active > 0) {
+        atomicAdd(&a.stats[kStatPasses], 1ull);
+        atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
+      }
+    }
+  }
+
+  auto enqueue = [&](uint32_t t, unsigned long long kb) {
+    atomicMin(&a.key_out[t], kb);
+    atomicMin(&s_minout, kb);
+    if (atomicMax(&a.tile_epoch[t], a.epoch) < a.epoch) {
+      atomicAdd(&s_hout[key_bin(bitsd(kb), origin_out, inv_delta)], 1u);
+      const uint32_t pos = atomicAdd(&s_nq, 1u);
+      if (pos < QCAP) {
+        s_q[pos] = t;
+      } else {
+        const uint32_t gp = atomicAdd(&a.count_out[shard], 1u);
+        a.list_out[(uint64_t)shard * a.shard_cap + gp] = t;
+      }
+    }
+  };
+
+  unsigned long long my_visits = 0, my_sweeps = 0;
+  double* img = s_img[wv];
+  unsigned long long* ek = s_ek[wv];
+  const uint32_t chunk = (n_active + gridDim.x - 1) / gridDim.x;
+  const uint32_t c0 = blockIdx.x * chunk;
+  const uint32_t c1 = min(n_active, c0 + chunk);
+  bool first = true;
+  if (trace && tid == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
+  for (;;) {  // wave-uniform
+    uint32_t e = 0;
+    if (lane == 0) e = c0 + atomicAdd(&s_next, 1u);
+    e = __builtin_amdgcn_readfirstlane(e);
+    if (e >= c1) break;
+    const uint32_t tile = __builtin_amdgcn_readfirstlane(list_at(a.list_in, a.shard_cap, s_pref, e));
+    const unsigned long long kb = a.key_in[tile];
+    const int tx = (int)(tile % (uint32_t)a.ntx);
+    const int ty = (int)(tile / (uint32_t)a.ntx);
+    if (lane < 4) ek[lane] = kInfBits;
+    if (trace && tid == 0 && first) trace[6] = __builtin_amdgcn_s_memrealtime();
+    bool capped = false;
+    const int sweeps = visit16(a, img, ek, true, tx, ty, lane, capped, [&] {
+      return key_bin(bitsd(kb), origin_in, inv_delta) <= bstar;
+    });
+    if (lane == 0) a.key_in[tile] = kInfBits;
+    if (sweeps < 0) {  // deferred to the next pass with its key
+      if (lane == 0) enqueue(tile, kb);
+      continue;
+    }
+    if (trace && tid == 0 && first) {
+      __builtin_amdgcn_s_waitcnt(0);
+      trace[7] = __builtin_amdgcn_s_memrealtime();
+      trace[9] = (unsigned long long)sweeps;
+    }
+    my_visits += 1;
+    my_sweeps += (unsigned long long)sweeps;
+    const bool cap = __any(capped);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    bool want = false;
+    int nx_t = tx, ny_t = ty;
+    unsigned long long k2 = kInfBits;
+    if (lane < 4) {
+      k2 = ek[lane];
+      if (lane == 0) { want = k2 != kInfBits && ty > 0; ny_t = ty - 1; }
+      else if (lane == 1) { want = k2 != kInfBits && tx > 0; nx_t = tx - 1; }
+      else if (lane == 2) { want = k2 != kInfBits && tx + 1 < a.ntx; nx_t = tx + 1; }
+      else { want = k2 != kInfBits && ty + 1 < a.nty; ny_t = ty + 1; }
+    } else if (lane == 4 && cap) {
+      want = true;
+      k2 = kb;
+    }
+    if (want) enqueue((uint32_t)ny_t * (uint32_t)a.ntx + (uint32_t)nx_t, k2);
+    __builtin_amdgcn_wave_barrier();
+    if (trace && first) {
+      __builtin_amdgcn_s_waitcnt(0);
+      if (tid == 0) trace[8] = __builtin_amdgcn_s_memrealtime();
+    }
+    first = false;
+  }
+  if (trace && tid == 0) trace[3] = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && my_visits) {
     atomicAdd(&s_visits, my_visits);
     atomicAdd(&s_sweeps, my_sweeps);
   }
@@ -1399,13 +1587,67 @@ hipError_t launch_pass_prio(const PassArgs& a, int blocks, hipStream_t st, hipEv
   return hipGetLastError();
 }
 
-hipError_t launch_pass_prio16(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
-                              hipEvent_t e1) {
+template <int WPB>
+hipError_t launch_prio16_wpb(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
+                             hipEvent_t e1) {
   if (e0 || e1)
-    hipExtLaunchKernelGGL(k_fim_pass_prio<16>, dim3(blocks), dim3(256), 0, st, e0, e1, 0, a);
+    hipExtLaunchKernelGGL((k_fim_pass_prio<16, WPB>), dim3(blocks), dim3(64 * WPB), 0, st, e0, e1,
+                          0, a);
   else
-    hipLaunchKernelGGL(k_fim_pass_prio<16>, dim3(blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_fim_pass_prio<16, WPB>), dim3(blocks), dim3(64 * WPB), 0, st, a);
   return hipGetLastError();
+}
+
+template <int WPB>
+hipError_t launch_dyn_wpb(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
+                          hipEvent_t e1) {
+  if (e0 || e1)
+    hipExtLaunchKernelGGL((k_fim_pass_dyn<WPB>), dim3(blocks), dim3(64 * WPB), 0, st, e0, e1, 0,
+                          a);
+  else
+    hipLaunchKernelGGL((k_fim_pass_dyn<WPB>), dim3(blocks), dim3(64 * WPB), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_pass_prio16(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
+                              hipEvent_t e1, int wpb, int dyn) {
+  if (dyn) switch (wpb) {
+      case 8: return launch_dyn_wpb<8>(a, blocks, st, e0, e1);
+      case 16: return launch_dyn_wpb<16>(a, blocks, st, e0, e1);
+      default: return launch_dyn_wpb<4>(a, blocks, st, e0, e1);
+    }
+  switch (wpb) {
+    case 8: return launch_prio16_wpb<8>(a, blocks, st, e0, e1);
+    case 16: return launch_prio16_wpb<16>(a, blocks, st, e0, e1);
+    default: return launch_prio16_wpb<4>(a, blocks, st, e0, e1);
+  }
+}
+
+int prio16_blocks_per_cu(int wpb, int dyn) {
+  int n = 0;
+  hipError_t e = hipErrorInvalidValue;
+  if (dyn) switch (wpb) {
+      case 8:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_dyn<8>, 512, 0);
+        break;
+      case 16:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_dyn<16>, 1024, 0);
+        break;
+      default:
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_dyn<4>, 256, 0);
+    }
+  else switch (wpb) {
+    case 8:
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_prio<16, 8>, 512, 0);
+      break;
+    case 16:
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_prio<16, 16>, 1024, 0);
+      break;
+    default:
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_prio<16, 4>, 256, 0);
+  }
+  (void)hipGetLastError();
+  return (e == hipSuccess && n > 0) ? n : 1;
 }
 
 int pass_blocks_per_cu(int variant) {
