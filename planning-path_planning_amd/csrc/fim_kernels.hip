@@ -443,6 +443,26 @@ __device__ __forceinline__ double sqrt_cr_fast(double x) {
   s = __builtin_fma(d, h, s);
   return s;
 }
+
+// sqrt_cr_fast on two independent operands, step-interleaved so the two
+// dependent chains overlap in a single wave (same operations: bit-identical)
+__device__ __forceinline__ void sqrt_cr_fast2(double x0, double x1, double& r0, double& r1) {
+  const double y0 = __builtin_amdgcn_rsq(x0), y1 = __builtin_amdgcn_rsq(x1);
+  double s0 = x0 * y0, s1 = x1 * y1;
+  double h0 = y0 * 0.5, h1 = y1 * 0.5;
+  const double e0 = __builtin_fma(-h0, s0, 0.5), e1 = __builtin_fma(-h1, s1, 0.5);
+  s0 = __builtin_fma(s0, e0, s0);
+  s1 = __builtin_fma(s1, e1, s1);
+  h0 = __builtin_fma(h0, e0, h0);
+  h1 = __builtin_fma(h1, e1, h1);
+  double d0 = __builtin_fma(-s0, s0, x0), d1 = __builtin_fma(-s1, s1, x1);
+  s0 = __builtin_fma(d0, h0, s0);
+  s1 = __builtin_fma(d1, h1, s1);
+  d0 = __builtin_fma(-s0, s0, x0);
+  d1 = __builtin_fma(-s1, s1, x1);
+  r0 = __builtin_fma(d0, h0, s0);
+  r1 = __builtin_fma(d1, h1, s1);
+}
 constexpr double kFastMinF = 0x1p-383;
 
 // One cell of the reference update (:504-537) against the image.  Preconditions
@@ -831,21 +851,33 @@ __device__ __forceinline__ int visit8(const PassArgs& a, double* img, unsigned l
 // NaN from a negative radicand; it is never selected).
 template <bool FAST, int PITCH>
 __device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, double f0,
-                                           double f1, double k10, double k11, double c20,
-                                           double c21, double& t0, double& t1, bool& ch0,
+                                           double f1, double& t0, double& t1, bool& ch0,
                                            bool& ch1) {
-  const double tx0 = vmin64(img[s0 - 1], img[s0 + 1]);
-  const double ty0 = vmin64(img[s0 + PITCH], img[s0 - PITCH]);
-  const double tx1 = vmin64(img[s1 - 1], img[s1 + 1]);
-  const double ty1 = vmin64(img[s1 + PITCH], img[s1 - PITCH]);
+  // all eight neighbour reads in flight before the first use
+  double w0 = img[s0 - 1], e0 = img[s0 + 1], n0 = img[s0 + PITCH], so0 = img[s0 - PITCH];
+  double w1 = img[s1 - 1], e1 = img[s1 + 1], n1 = img[s1 + PITCH], so1 = img[s1 - PITCH];
+  // one wait for all eight (the v_min asm below would otherwise pin reads behind it)
+  asm volatile("" : "+v"(w0), "+v"(e0), "+v"(n0), "+v"(so0), "+v"(w1), "+v"(e1), "+v"(n1),
+               "+v"(so1));
+  // per-cell constants: the compiler hoists them out of the sweep loop (held
+  // live there, measured faster than recomputing them under the LDS wait)
+  const double k10 = 0.7071 * f0, k11 = 0.7071 * f1;
+  const double c20 = 2.0 * (f0 * f0), c21 = 2.0 * (f1 * f1);
+  const double tx0 = vmin64(w0, e0), ty0 = vmin64(n0, so0);
+  const double tx1 = vmin64(w1, e1), ty1 = vmin64(n1, so1);
   const double m0 = vmin64(tx0, ty0), m1 = vmin64(tx1, ty1);
   const bool need0 = m0 + k10 < t0, need1 = m1 + k11 < t1;
   ch0 = ch1 = false;
   if (__any(need0 || need1)) {  // wave-uniform
     const double d0 = tx0 - ty0, d1 = tx1 - ty1;
     const double r0 = c20 - d0 * d0, r1 = c21 - d1 * d1;
-    const double q0 = FAST ? sqrt_cr_fast(r0) : sqrt(r0);
-    const double q1 = FAST ? sqrt_cr_fast(r1) : sqrt(r1);
+    double q0, q1;
+    if constexpr (FAST) {
+      sqrt_cr_fast2(r0, r1, q0, q1);
+    } else {
+      q0 = sqrt(r0);
+      q1 = sqrt(r1);
+    }
     const double u0 = fabs(d0) < f0 ? ((tx0 + ty0) + q0) * 0.5 : m0 + f0;
     const double u1 = fabs(d1) < f1 ? ((tx1 + ty1) + q1) * 0.5 : m1 + f1;
     ch0 = need0 && u0 < t0;
@@ -860,26 +892,16 @@ __device__ __forceinline__ int rb_sweeps4(double* img, const int (&sr)[2], const
                                           const double (&fr)[2], const double (&fb)[2],
                                           double (&tr)[2], double (&tb)[2], int max_inner,
                                           bool& capped) {
-  double k1r[2], k1b[2], c2r[2], c2b[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    k1r[k] = 0.7071 * fr[k];
-    k1b[k] = 0.7071 * fb[k];
-    c2r[k] = 2.0 * (fr[k] * fr[k]);
-    c2b[k] = 2.0 * (fb[k] * fb[k]);
-  }
   int sweeps = 0;
   capped = true;
   while (sweeps < max_inner) {
     __builtin_amdgcn_wave_barrier();
     bool i0, i1, i2, i3;
-    rb_update2<FAST, IP16>(img, sr[0], sr[1], fr[0], fr[1], k1r[0], k1r[1], c2r[0], c2r[1],
-                           tr[0], tr[1], i0, i1);
+    rb_update2<FAST, IP16>(img, sr[0], sr[1], fr[0], fr[1], tr[0], tr[1], i0, i1);
     img[sr[0]] = tr[0];
     img[sr[1]] = tr[1];
     __builtin_amdgcn_wave_barrier();
-    rb_update2<FAST, IP16>(img, sb[0], sb[1], fb[0], fb[1], k1b[0], k1b[1], c2b[0], c2b[1],
-                           tb[0], tb[1], i2, i3);
+    rb_update2<FAST, IP16>(img, sb[0], sb[1], fb[0], fb[1], tb[0], tb[1], i2, i3);
     img[sb[0]] = tb[0];
     img[sb[1]] = tb[1];
     ++sweeps;
@@ -964,8 +986,9 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
   const double tr0[2] = {tr[0], tr[1]}, tb0[2] = {tb[0], tb[1]};
   const bool fast = __all(!(fr[0] < kFastMinF) && !(fr[1] < kFastMinF) &&
                           !(fb[0] < kFastMinF) && !(fb[1] < kFastMinF));
-  const int sweeps = fast ? rb_sweeps4<true>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped)
-                          : rb_sweeps4<false>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped);
+  const int sweeps =
+      fast ? rb_sweeps4<true>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped)
+           : rb_sweeps4<false>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped);
   unsigned long long v[4];  // cells 4q..4q+3 in column order, decreased value or +inf
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
