@@ -417,6 +417,9 @@ __global__ __launch_bounds__(256) void k_fim_pass_w8(PassArgs a) {
 // and 16 distinct ds_write_b64 banks per 16-lane group (pitch 10 was 2-way).
 constexpr int IP = 12;
 constexpr int IP16 = 20;  // 16x16 image pitch (18 + 2)
+#ifndef DYMU_GATE
+#define DYMU_GATE 0
+#endif
 
 // v_min_f64 on operands that are never NaN (T >= 0 or +inf): one instruction,
 // no canonicalisation (the compiler cannot prove no-NaN for fmin).
@@ -859,6 +862,7 @@ __device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, do
   // one wait for all eight (the v_min asm below would otherwise pin reads behind it)
   asm volatile("" : "+v"(w0), "+v"(e0), "+v"(n0), "+v"(so0), "+v"(w1), "+v"(e1), "+v"(n1),
                "+v"(so1));
+#if DYMU_GATE
   // per-cell constants: the compiler hoists them out of the sweep loop (held
   // live there, measured faster than recomputing them under the LDS wait)
   const double k10 = 0.7071 * f0, k11 = 0.7071 * f1;
@@ -869,6 +873,17 @@ __device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, do
   const bool need0 = m0 + k10 < t0, need1 = m1 + k11 < t1;
   ch0 = ch1 = false;
   if (__any(need0 || need1)) {  // wave-uniform
+#else
+  // No skip test: u < t alone decides (u >= min + C/sqrt(2) > min + 0.7071 C, so
+  // the skip test of rb_update never rejects an improving candidate), and the
+  // half-sweep is one straight-line dependent chain without a scalar branch.
+  const double c20 = 2.0 * (f0 * f0), c21 = 2.0 * (f1 * f1);
+  const double tx0 = vmin64(w0, e0), ty0 = vmin64(n0, so0);
+  const double tx1 = vmin64(w1, e1), ty1 = vmin64(n1, so1);
+  const double m0 = vmin64(tx0, ty0), m1 = vmin64(tx1, ty1);
+  constexpr bool need0 = true, need1 = true;
+  {
+#endif
     const double d0 = tx0 - ty0, d1 = tx1 - ty1;
     const double r0 = c20 - d0 * d0, r1 = c21 - d1 * d1;
     double q0, q1;
