@@ -417,6 +417,9 @@ __global__ __launch_bounds__(256) void k_fim_pass_w8(PassArgs a) {
 // and 16 distinct ds_write_b64 banks per 16-lane group (pitch 10 was 2-way).
 constexpr int IP = 12;
 constexpr int IP16 = 20;  // 16x16 image pitch (18 + 2)
+#ifndef DYMU_CHECK2
+#define DYMU_CHECK2 1
+#endif
 #ifndef DYMU_GATE
 #define DYMU_GATE 0
 #endif
@@ -897,8 +900,15 @@ __device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, do
     const double u1 = fabs(d1) < f1 ? ((tx1 + ty1) + q1) * 0.5 : m1 + f1;
     ch0 = need0 && u0 < t0;
     ch1 = need1 && u1 < t1;
+#if DYMU_GATE
     t0 = ch0 ? u0 : t0;
     t1 = ch1 ? u1 : t1;
+#else
+    // min(t, u) == (u < t ? u : t): one v_min_f64 on the chain to the LDS write
+    // (a NaN candidate -- obstacle cells on the FAST path -- leaves t, as v_min does)
+    t0 = vmin64(t0, u0);
+    t1 = vmin64(t1, u1);
+#endif
   }
 }
 
@@ -910,8 +920,21 @@ __device__ __forceinline__ int rb_sweeps4(double* img, const int (&sr)[2], const
   int sweeps = 0;
   capped = true;
   while (sweeps < max_inner) {
-    __builtin_amdgcn_wave_barrier();
     bool i0, i1, i2, i3;
+#if DYMU_CHECK2
+    // two sweeps per convergence test: the second sweep's flags decide (a sweep
+    // that changes nothing is the local fixed point)
+    __builtin_amdgcn_wave_barrier();
+    rb_update2<FAST, IP16>(img, sr[0], sr[1], fr[0], fr[1], tr[0], tr[1], i0, i1);
+    img[sr[0]] = tr[0];
+    img[sr[1]] = tr[1];
+    __builtin_amdgcn_wave_barrier();
+    rb_update2<FAST, IP16>(img, sb[0], sb[1], fb[0], fb[1], tb[0], tb[1], i2, i3);
+    img[sb[0]] = tb[0];
+    img[sb[1]] = tb[1];
+    ++sweeps;
+#endif
+    __builtin_amdgcn_wave_barrier();
     rb_update2<FAST, IP16>(img, sr[0], sr[1], fr[0], fr[1], tr[0], tr[1], i0, i1);
     img[sr[0]] = tr[0];
     img[sr[1]] = tr[1];
