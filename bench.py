@@ -8,8 +8,9 @@ propagation: T initialised, relaxed to convergence, result in HBM).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--size S] [--obst P]
 
 N > 1 runs under torch.distributed.run, one rank per GPU: the grid is cut in
-row slabs, one per rank, with RCCL halo exchange (dymu_sharded_*); value is
-the whole-job rate N^2 / max-over-ranks solve time.
+row slabs, one per rank, with RCCL halo exchange driven from C++
+(include/dymu_dist.h; bench_sharded.py); value is the whole-job rate
+N^2 / max-over-ranks solve time.
 
 Rank 0 prints ONE JSON line with the roofline of the dominant kernel
 (k_fim_pass, per-launch HIP events over the timed region) and the CPU baseline
@@ -46,6 +47,9 @@ def parse():
                     help="no per-launch events (roofline reported as null)")
     ap.add_argument("--backend", default="nccl",
                     help="N>1 only: 'nccl' (RCCL over xGMI) or 'gloo' (host-staged rehearsal)")
+    ap.add_argument("--exchange", default="native", choices=["native", "python"],
+                    help="N>1: 'native' = C++ exchange loop with its own RCCL communicator "
+                         "(libdymu_dist); 'python' = dymu.sharded over torch.distributed")
     ap.add_argument("--passes-per-exchange", type=int, default=16)
     ap.add_argument("--sharded", action="store_true",
                     help="run the row-slab path even at N=1 (exercises the RCCL code path)")
@@ -195,7 +199,10 @@ def main():
             "workload": f"config 3: {N}x{N} grid, {world}x MI355X, splitmix64 U(1,5) speed, "
                         f"{args.obst:.0%} iid obstacles, goal centre, full solve",
             "grid": N,
-            "parallelism": "single" if world == 1 else f"row-slab x{world} ({args.backend})",
+            "parallelism": ("single" if world == 1 and not args.sharded else
+                            f"row-slab x{world} ("
+                            + ("RCCL, native C++ loop" if args.exchange == "native"
+                               else f"{args.backend}, torch.distributed loop") + ")"),
             "exchange_rounds_per_solve": tot.get("rounds", 0) / K,
             "passes_per_solve": tot["passes"] / K,
             "tile_visits_per_solve": tot["tile_visits"] / K,

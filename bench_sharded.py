@@ -1,7 +1,13 @@
 """Multi-GPU leg of bench.py: one rank per GPU (torch.distributed.run), the
-16384^2 grid split in row slabs (dymu.slab_rows), solved by
-dymu.sharded.SlabSolver with boundary-row exchange over RCCL ('nccl').
-`--backend gloo` rehearses N ranks on one GPU with host-staged rows."""
+16384^2 grid split in row slabs (dymu.slab_rows).
+
+--exchange native (default): the C++ loop of libdymu_dist (dymu.dist.DistSolver)
+    with its own RCCL communicator on the engine's stream; torch.distributed
+    (gloo) only carries the communicator id, barriers and the max-over-ranks time.
+--exchange python: dymu.sharded.SlabSolver, the exchange loop in Python over
+    torch.distributed ('nccl' = RCCL, or `--backend gloo` to rehearse N ranks on
+    one GPU with host-staged rows).
+"""
 import os
 import time
 
@@ -9,16 +15,26 @@ import torch  # noqa: F401  (first: one HIP runtime for torch and libdymu_fim)
 import torch.distributed as dist
 
 import dymu
-from dymu.sharded import SlabSolver
 
 PROFILE_PERIOD = 8  # time every 8th pass launch of rank 0 (bench.py's roofline)
 
 
+def _env_defaults():
+    # `bench.py --sharded` without torchrun: a world of one
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    os.environ.setdefault("LOCAL_RANK", "0")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+
+
 def run(args):
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    backend = getattr(args, "backend", "nccl")
+    _env_defaults()
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ["LOCAL_RANK"])
+    native = getattr(args, "exchange", "native") == "native"
+    backend = "gloo" if native else getattr(args, "backend", "nccl")
     ngpu = torch.cuda.device_count()
     dev_idx = local % max(ngpu, 1)
     torch.cuda.set_device(dev_idx)
@@ -35,10 +51,27 @@ def run(args):
     T_buf = torch.empty((nrows + 2, N), dtype=torch.float64, device=device)
     stream = torch.cuda.current_stream(device).cuda_stream
     eng.synth_speed(F.data_ptr(), N, nrows, N, row0, 1, args.obst, 3, g[0], g[1], stream)
-    solver = SlabSolver(eng, N, N, rank, world, row0, nrows, device,
-                        passes_per_exchange=args.passes_per_exchange, check_every=4)
+    torch.cuda.synchronize()
+    if native:
+        from dymu import dist as ddist
+
+        obj = [ddist.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        solver = ddist.DistSolver(eng, dev_idx, obj[0], rank, world)
+
+        def solve():
+            return solver.solve(F.data_ptr(), T_buf.data_ptr(), N, N, N, g[0], g[1],
+                                args.passes_per_exchange)
+    else:
+        from dymu.sharded import SlabSolver
+
+        solver = SlabSolver(eng, N, N, rank, world, row0, nrows, device,
+                            passes_per_exchange=args.passes_per_exchange, check_every=4)
+
+        def solve():
+            return solver.solve(F, T_buf, g[0], g[1])
     for _ in range(args.warmup):
-        solver.solve(F, T_buf, g[0], g[1])
+        solve()
     prof = not args.no_profile
     eng.set_profiling(PROFILE_PERIOD if prof else 0)
     kern_ms, kern_n = 0.0, 0
@@ -47,7 +80,7 @@ def run(args):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        st = solver.solve(F, T_buf, g[0], g[1])
+        st = solve()
         for k in tot:
             tot[k] += st[k]
         if prof:
@@ -59,6 +92,9 @@ def run(args):
     dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
                       device=device if backend == "nccl" else "cpu")
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    if os.environ.get("DYMU_BENCH_VERBOSE"):
+        print(f"rank {rank}: rows {row0}+{nrows} {tot} {time.perf_counter() - t0:.4f}s",
+              flush=True)
     tot["rank0_tile_visits"] = tot["tile_visits"]  # this rank's (rank 0 reports)
     agg = torch.tensor([tot["tile_visits"], tot["inner_sweeps"], tot["passes"]],
                        dtype=torch.float64, device=dt.device)
@@ -67,6 +103,8 @@ def run(args):
     tot["passes_sum_ranks"] = int(agg[2])
     tot["slab_cells"] = nrows * N  # rank 0's slab: the roofline's per-launch bytes
     eng.set_profiling(0)
+    if native:
+        solver.close()
     eng.close()
     dist.destroy_process_group()
     if rank != 0:

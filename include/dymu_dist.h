@@ -1,0 +1,76 @@
+/*
+ * dymu_dist.h -- C-ABI of the row-slab sharded solve driven natively (C++
+ * loop, RCCL over xGMI on the engine's stream).
+ *
+ * One process per GPU.  The global ny x nx grid is cut into row slabs
+ * (dymu_slab_rows); rank r owns rows [row0, row0+nrows) and solves them with
+ * the engine's domain primitives (dymu_dom_*, include/dymu_fim.h).  Every
+ * `passes_per_exchange` passes the ranks swap their boundary rows with
+ * rank-1 / rank+1 (grouped ncclSend/ncclRecv, 2 x nx x 8 B per neighbour),
+ * min-merge them into their ghost rows, and all-reduce the number of queued
+ * tiles (4 bytes).  The host never waits for the exchange it just queued: it
+ * reads the all-reduced count of the PREVIOUS exchange round (pinned host
+ * copy + event), so the device always has one round of work queued.  A zero
+ * count means the global fixed point was reached.
+ *
+ * This replaces, for a grid too large or too slow for one GPU, the reference's
+ * single-threaded propagation loop computeEntireTotalCostMap
+ * (src/DyMu_GlobalPathPlanning.cpp:443-468); the result is the single-GPU
+ * fixed point (values only decrease; ghost rows are valid upper bounds).
+ *
+ * Slab buffers (device, pitch ld >= nx):
+ *   F_slab: nrows rows (the rank's rows of F)
+ *   T_buf:  nrows + 2 rows; row 0 = ghost row (rank-1's last row), rows
+ *           1..nrows = owned rows, row nrows+1 = ghost row (rank+1's first row)
+ */
+#ifndef DYMU_DIST_H
+#define DYMU_DIST_H
+
+#include <stdint.h>
+
+#include "dymu_fim.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DYMU_DIST_ID_BYTES 128 /* sizeof(ncclUniqueId) */
+
+typedef struct dymu_dist dymu_dist;
+
+/* Rank 0 creates the communicator id; the caller broadcasts the 128 bytes
+ * (e.g. torch.distributed over TCP/gloo) to every rank. */
+int dymu_dist_unique_id(unsigned char id[DYMU_DIST_ID_BYTES]);
+
+/* Collective over the `world` ranks: creates the RCCL communicator on `device`
+ * (the device of `ctx`).  `ctx` stays owned by the caller and must outlive the
+ * dymu_dist. */
+int dymu_dist_create(dymu_dist** out, dymu_ctx* ctx, int device,
+                     const unsigned char id[DYMU_DIST_ID_BYTES], int rank, int world);
+int dymu_dist_destroy(dymu_dist* d);
+
+/* Sharded solve of the global grid (nx x ny, goal (goal_i, goal_j) in global
+ * coordinates); this rank's slab geometry comes from dymu_slab_rows.
+ * Collective: every rank calls it with the same nx, ny, goal and
+ * passes_per_exchange (0 = 16).  `stream` NULL = the context's stream.
+ * Blocks until converged; stats are this rank's (rounds = exchange rounds). */
+int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t ld, uint32_t nx,
+                    uint32_t ny, uint32_t goal_i, uint32_t goal_j, uint32_t passes_per_exchange,
+                    void* stream, dymu_stats* stats);
+
+/* The same loop with `world` virtual ranks in one process (tests, rehearsal):
+ * ctxs[r] / F_slabs[r] / T_bufs[r] are rank r's context and slab buffers, all
+ * on the current device; the exchange is device-to-device copies and the
+ * all-reduce a host sum, all ordered on `stream` (required, not NULL).
+ * stats: `world` entries (may be NULL). */
+int dymu_vdist_solve(dymu_ctx* const* ctxs, int world, const double* const* F_slabs,
+                     double* const* T_bufs, uint64_t ld, uint32_t nx, uint32_t ny,
+                     uint32_t goal_i, uint32_t goal_j, uint32_t passes_per_exchange,
+                     void* stream, dymu_stats* stats);
+
+const char* dymu_dist_last_error(dymu_dist* d);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

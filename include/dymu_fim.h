@@ -217,6 +217,9 @@ int dymu_set_profiling(dymu_ctx* ctx, int period);
  * pass_ms_total / n_pass_launches -- the bench's roofline source. */
 int dymu_last_pass_timing(dymu_ctx* ctx, double* pass_ms_total, uint64_t* n_pass_launches);
 
+/* The context's own stream (the hipStream_t that NULL `stream` arguments mean). */
+void* dymu_get_stream(dymu_ctx* ctx);
+
 const char* dymu_strerror(int status);
 const char* dymu_last_error(dymu_ctx* ctx); /* last HIP/RCCL error text */
 int dymu_abi_version(void);

@@ -510,6 +510,8 @@ int dymu_device_count(void) {
   return n;
 }
 
+void* dymu_get_stream(dymu_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+
 const char* dymu_strerror(int s) {
   switch (s) {
     case DYMU_OK: return "ok";

@@ -5,6 +5,8 @@ Thin ctypes layer over the two in-tree shared libraries:
 * ``lib/libdymu_fim.so``     -- HIP kernels + C-ABI (include/dymu_fim.h)
 * ``lib/libdymu_planner.so`` -- host C++ ``PathPlanning_lib::DyMuPathPlanner``
                                 (include/DyMu.hpp) behind include/dymu_planner.h
+* ``lib/libdymu_dist.so``    -- row-slab sharded solve over RCCL
+                                (include/dymu_dist.h; binding in dymu.dist)
 
 There is no CPU fallback: if the HIP library is missing or no device is
 visible, every entry point raises ``DymuError``.  The CPU oracle under
@@ -125,6 +127,7 @@ FIM_SYMBOLS = {
                                           _u32, _u32, _u32, _vp, ctypes.POINTER(DymuStats)]),
     "dymu_resolve_window": (_i32, [_vp, _dp, _u32, _u32, _u32, _u32, _u32, _u32, _u32, _u32,
                                    _dp, ctypes.POINTER(DymuStats)]),
+    "dymu_get_stream": (_vp, [_vp]),
     "dymu_strerror": (ctypes.c_char_p, [_i32]),
     "dymu_last_error": (ctypes.c_char_p, [_vp]),
     "dymu_abi_version": (_i32, []),

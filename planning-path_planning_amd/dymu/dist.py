@@ -1,0 +1,114 @@
+"""Row-slab sharded solve driven natively (libdymu_dist.so, include/dymu_dist.h).
+
+The exchange loop of dymu.sharded.SlabSolver, moved into C++ on the engine's
+stream: K passes -> grouped ncclSend/ncclRecv of the boundary rows with rank±1
+(RCCL over xGMI) -> min-merge into the ghost rows -> ncclAllReduce of the queued
+tile count, read back one round late so the host never drains the device queue.
+
+torch.distributed only carries the control plane here (the 128-byte RCCL
+communicator id, barriers, timing); the data path is the library's own RCCL
+communicator.  `VirtualWorld` runs the same loop with N slabs in one process on
+one GPU (device-to-device copies instead of RCCL) for the tests.
+
+Reference: computeEntireTotalCostMap's propagation loop
+(src/DyMu_GlobalPathPlanning.cpp:443-468), distributed as SURVEY.md s8(e).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from . import DymuError, DymuStats, _check, lib_path, load_fim
+
+_i32, _u32, _u64, _vp = ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p
+ID_BYTES = 128
+
+DIST_SYMBOLS = {
+    "dymu_dist_unique_id": (_i32, [ctypes.c_char_p]),
+    "dymu_dist_create": (_i32, [ctypes.POINTER(_vp), _vp, _i32, ctypes.c_char_p, _i32, _i32]),
+    "dymu_dist_destroy": (_i32, [_vp]),
+    "dymu_dist_solve": (_i32, [_vp, _vp, _vp, _u64, _u32, _u32, _u32, _u32, _u32, _vp,
+                               ctypes.POINTER(DymuStats)]),
+    "dymu_vdist_solve": (_i32, [ctypes.POINTER(_vp), _i32, ctypes.POINTER(_vp),
+                                ctypes.POINTER(_vp), _u64, _u32, _u32, _u32, _u32, _u32, _vp,
+                                ctypes.POINTER(DymuStats)]),
+    "dymu_dist_last_error": (ctypes.c_char_p, [_vp]),
+}
+
+_dl = None
+
+
+def load_dist() -> ctypes.CDLL:
+    global _dl
+    if _dl is None:
+        load_fim()
+        path = lib_path("libdymu_dist.so")
+        if not os.path.exists(path):
+            raise DymuError(-5, f"dist library missing: {path} (run __graft_entry__.build())")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in DIST_SYMBOLS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _dl = lib
+    return _dl
+
+
+def unique_id() -> bytes:
+    """A fresh RCCL communicator id (call on rank 0, broadcast the bytes)."""
+    buf = ctypes.create_string_buffer(ID_BYTES)
+    _check(load_dist().dymu_dist_unique_id(buf))
+    return buf.raw
+
+
+class DistSolver:
+    """One rank of the native sharded solver.  Collective construction."""
+
+    def __init__(self, engine, device: int, uid: bytes, rank: int, world: int):
+        assert len(uid) == ID_BYTES
+        self._lib = load_dist()
+        self.eng = engine
+        self.rank, self.world = rank, world
+        self.h = _vp()
+        rc = self._lib.dymu_dist_create(ctypes.byref(self.h), engine.ctx, device, uid, rank,
+                                        world)
+        if rc != 0:
+            raise DymuError(rc, "dymu_dist_create (RCCL communicator)")
+
+    def close(self):
+        if self.h:
+            self._lib.dymu_dist_destroy(self.h)
+            self.h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def solve(self, F_slab: int, T_buf: int, ld: int, nx: int, ny: int, goal_i: int,
+              goal_j: int, passes_per_exchange: int = 16, stream: int = 0) -> dict:
+        """F_slab: this rank's rows; T_buf: nrows + 2 rows (ghost, owned..., ghost)."""
+        st = DymuStats()
+        rc = self._lib.dymu_dist_solve(self.h, F_slab, T_buf, ld, nx, ny, goal_i, goal_j,
+                                       passes_per_exchange, stream or None, ctypes.byref(st))
+        if rc != 0:
+            msg = self._lib.dymu_dist_last_error(self.h)
+            raise DymuError(rc, msg.decode() if msg else "")
+        return st.as_dict()
+
+
+def vdist_solve(engines, F_slabs, T_bufs, ld: int, nx: int, ny: int, goal_i: int, goal_j: int,
+                passes_per_exchange: int = 16, stream: int = 0) -> list:
+    """All ranks in one process on one GPU (the C++ loop with copies for RCCL)."""
+    lib = load_dist()
+    w = len(engines)
+    ctxs = (_vp * w)(*[e.ctx for e in engines])
+    Fp = (_vp * w)(*F_slabs)
+    Tp = (_vp * w)(*T_bufs)
+    stats = (DymuStats * w)()
+    if not stream:
+        stream = load_fim().dymu_get_stream(engines[0].ctx)
+    _check(lib.dymu_vdist_solve(ctxs, w, Fp, Tp, ld, nx, ny, goal_i, goal_j,
+                                passes_per_exchange, stream, stats))
+    return [s.as_dict() for s in stats]

@@ -35,6 +35,28 @@ def test_planner_exports_every_declared_symbol(dymu):
     assert set(names) <= set(dymu.PLANNER_SYMBOLS), set(names) - set(dymu.PLANNER_SYMBOLS)
 
 
+def test_dist_exports_every_declared_symbol(dymu):
+    from dymu import dist
+
+    lib = dist.load_dist()
+    names = [n for n in declared("dymu_dist.h")]
+    assert len(names) >= 6
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) <= set(dist.DIST_SYMBOLS), set(names) - set(dist.DIST_SYMBOLS)
+
+
+def test_dist_rejects_bad_arguments(dymu):
+    """Argument checks run before any device or RCCL call."""
+    from dymu import dist
+
+    lib = dist.load_dist()
+    h = ctypes.c_void_p()
+    assert lib.dymu_dist_create(ctypes.byref(h), None, 0, b"\0" * 128, 0, 1) == -1
+    assert lib.dymu_dist_solve(None, None, None, 0, 8, 8, 0, 0, 0, None, None) == -1
+    assert lib.dymu_vdist_solve(None, 2, None, None, 8, 8, 8, 0, 0, 0, None, None) == -1
+
+
 def test_abi_version_and_strerror(dymu):
     lib = dymu.load_fim()
     assert lib.dymu_abi_version() == 2
@@ -68,7 +90,8 @@ def test_planner_solve_refuses_without_device(dymu):
 def test_headers_compile_as_c_and_cpp(tmp_path):
     """The C-ABI headers are plain C; DyMu.hpp builds without Rock."""
     c = tmp_path / "t.c"
-    c.write_text('#include "dymu_fim.h"\n#include "dymu_planner.h"\nint main(void){return 0;}\n')
+    c.write_text('#include "dymu_fim.h"\n#include "dymu_planner.h"\n#include "dymu_dist.h"\n'
+                 'int main(void){return 0;}\n')
     cc = tmp_path / "t.cpp"
     cc.write_text('#include "DyMu.hpp"\nint main(){PathPlanning_lib::DyMuPathPlanner p(1,1,1,'
                   'PathPlanning_lib::CONSERVATIVE);return 0;}\n')

@@ -74,3 +74,35 @@ def test_gpu_sharded_matches_oracle(oracle, world, nx, ny, goal, engine_kw):
     assert np.array_equal(np.isinf(T), np.isinf(Tref))
     fin = np.isfinite(Tref)
     assert (np.abs(T[fin] - Tref[fin]) / np.maximum(1, Tref[fin])).max() <= 1e-12
+
+
+@pytest.mark.parametrize("engine_kw", [dict(kernel=3), dict(kernel=5, prio_target=8)],
+                         ids=["fim", "prio16"])
+def test_native_rccl_world1_matches_oracle(dymu, oracle, engine_kw):
+    """libdymu_dist's RCCL path in-process with a one-rank communicator
+    (ncclCommInitRank + the lagged all-reduce; no peers, so no P2P): the
+    native loop, the RCCL calls it makes at N=1 and its result vs the oracle.
+    Two ranks cannot share one GPU under RCCL ('Duplicate GPU'), so the P2P
+    rows are covered by dymu_vdist_solve (test_gpu_slabs.py) and gloo tests."""
+    from dymu import dist
+
+    nx, ny, goal = 203, 150, (31, 77)
+    F = oracle.synth_speed(nx, ny, seed=5, obst_frac=0.03, obst_seed=6, goal=goal)
+    eng = dymu.Engine(device=0, **engine_kw)
+    solver = dist.DistSolver(eng, 0, dist.unique_id(), 0, 1)
+    dF = eng.alloc(8 * nx * ny)
+    dT = eng.alloc(8 * (ny + 2) * nx)
+    eng.h2d(dF, F)
+    for _ in range(2):  # reuse of the communicator and the workspace
+        st = solver.solve(dF, dT, nx, nx, ny, goal[0], goal[1], 4)
+    T = np.empty((ny, nx))
+    eng.d2h(T, dT + 8 * nx)
+    solver.close()
+    eng.free(dF)
+    eng.free(dT)
+    eng.close()
+    Tref, _ = oracle.fmm(F, goal)
+    assert np.array_equal(np.isinf(T), np.isinf(Tref))
+    fin = np.isfinite(Tref)
+    assert (np.abs(T[fin] - Tref[fin]) / np.maximum(1, Tref[fin])).max() <= 1e-12
+    assert st["rounds"] >= 2 and st["passes"] > 0

@@ -70,3 +70,71 @@ def test_virtual_slabs_match_oracle(dymu, oracle, S, nx, ny, goal, frac, kw):
     fin = np.isfinite(Tref)
     assert (np.abs(T[fin] - Tref[fin]) / np.maximum(1, Tref[fin])).max() <= 1e-12
     assert rounds > 1
+
+
+def solve_vdist(dymu, F, goal, S, K=8, **engine_kw):
+    """The native C++ sharded loop (libdymu_dist, dymu_vdist_solve): S slabs on
+    one GPU, device-to-device row exchange, lagged termination check."""
+    from dymu import dist
+
+    ny, nx = F.shape
+    engs, dFs, dTs, geo = [], [], [], []
+    for s in range(S):
+        row0, nrows = dymu.slab_rows(ny, S, s)
+        eng = dymu.Engine(**engine_kw)
+        dF = eng.alloc(8 * nrows * nx)
+        dT = eng.alloc(8 * (nrows + 2) * nx)
+        eng.h2d(dF, np.ascontiguousarray(F[row0:row0 + nrows]))
+        engs.append(eng)
+        dFs.append(dF)
+        dTs.append(dT)
+        geo.append((row0, nrows))
+    stats = dist.vdist_solve(engs, dFs, dTs, nx, nx, ny, goal[0], goal[1], K)
+    T = np.empty((ny, nx))
+    for eng, dF, dT, (row0, nrows) in zip(engs, dFs, dTs, geo):
+        buf = np.empty((nrows, nx))
+        eng.d2h(buf, dT + 8 * nx)
+        T[row0:row0 + nrows] = buf
+        eng.free(dF)
+        eng.free(dT)
+        eng.close()
+    return T, stats
+
+
+@pytest.mark.parametrize("S,nx,ny,goal,frac,K", [(1, 96, 80, (10, 70), 0.02, 4),
+                                                 (2, 200, 160, (100, 40), 0.02, 8),
+                                                 (3, 130, 200, (7, 190), 0.05, 3),
+                                                 (4, 256, 256, (128, 128), 0.0, 16),
+                                                 (5, 64, 320, (32, 0), 0.03, 1)])
+@pytest.mark.parametrize("kw", [dict(kernel=3), dict(kernel=5, prio_target=8)],
+                         ids=["fim", "prio16"])
+def test_native_vdist_matches_oracle(dymu, oracle, S, nx, ny, goal, frac, K, kw):
+    F = oracle.synth_speed(nx, ny, seed=37, obst_frac=frac, obst_seed=9, goal=goal)
+    T, stats = solve_vdist(dymu, F, goal, S, K=K, **kw)
+    Tref, _ = oracle.fmm(F, goal)
+    assert np.array_equal(np.isinf(T), np.isinf(Tref))
+    fin = np.isfinite(Tref)
+    assert (np.abs(T[fin] - Tref[fin]) / np.maximum(1, Tref[fin])).max() <= 1e-12
+    assert len(stats) == S and all(st["rounds"] == stats[0]["rounds"] for st in stats)
+    assert stats[0]["rounds"] >= 2  # at least the converged round + the lagged one
+
+
+def test_native_vdist_large_matches_single(dymu):
+    """2048^2 with the default kernel choice: the stitched slabs equal the
+    single-GPU solve's fixed point (both within ulps of each other)."""
+    N, g = 2048, (700, 1500)
+    eng = dymu.Engine()
+    dF, dT = eng.alloc(8 * N * N), eng.alloc(8 * N * N)
+    eng.synth_speed(dF, N, N, N, 0, 1, 0.02, 3, g[0], g[1])
+    F = np.empty((N, N))
+    eng.d2h(F, dF)
+    eng.solve_device(dF, dT, N, N, N, g[0], g[1])
+    T1 = np.empty((N, N))
+    eng.d2h(T1, dT)
+    eng.free(dF)
+    eng.free(dT)
+    eng.close()
+    T, stats = solve_vdist(dymu, F, g, 4, K=16)
+    assert np.array_equal(np.isinf(T), np.isinf(T1))
+    fin = np.isfinite(T1)
+    assert (np.abs(T[fin] - T1[fin]) / np.maximum(1, T1[fin])).max() <= 1e-12
