@@ -34,6 +34,7 @@ def run(args):
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ["LOCAL_RANK"])
     native = getattr(args, "exchange", "native") == "native"
+    K = args.passes_per_exchange or (4 if native else 16)
     backend = "gloo" if native else getattr(args, "backend", "nccl")
     ngpu = torch.cuda.device_count()
     dev_idx = local % max(ngpu, 1)
@@ -60,13 +61,12 @@ def run(args):
         solver = ddist.DistSolver(eng, dev_idx, obj[0], rank, world)
 
         def solve():
-            return solver.solve(F.data_ptr(), T_buf.data_ptr(), N, N, N, g[0], g[1],
-                                args.passes_per_exchange)
+            return solver.solve(F.data_ptr(), T_buf.data_ptr(), N, N, N, g[0], g[1], K)
     else:
         from dymu.sharded import SlabSolver
 
         solver = SlabSolver(eng, N, N, rank, world, row0, nrows, device,
-                            passes_per_exchange=args.passes_per_exchange, check_every=4)
+                            passes_per_exchange=K, check_every=4)
 
         def solve():
             return solver.solve(F, T_buf, g[0], g[1])

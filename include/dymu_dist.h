@@ -5,13 +5,15 @@
  * One process per GPU.  The global ny x nx grid is cut into row slabs
  * (dymu_slab_rows); rank r owns rows [row0, row0+nrows) and solves them with
  * the engine's domain primitives (dymu_dom_*, include/dymu_fim.h).  Every
- * `passes_per_exchange` passes the ranks swap their boundary rows with
- * rank-1 / rank+1 (grouped ncclSend/ncclRecv, 2 x nx x 8 B per neighbour),
- * min-merge them into their ghost rows, and all-reduce the number of queued
- * tiles (4 bytes).  The host never waits for the exchange it just queued: it
- * reads the all-reduced count of the PREVIOUS exchange round (pinned host
- * copy + event), so the device always has one round of work queued.  A zero
- * count means the global fixed point was reached.
+ * `passes_per_exchange` passes (one round) a rank packs its two boundary rows
+ * and sends them to rank-1 / rank+1 (grouped ncclSend/ncclRecv, nx x 8 B per
+ * neighbour) together with an all-reduce of its queued-tile count (4 bytes),
+ * on a second stream: the transfer overlaps the next round's passes, and the
+ * rows are min-merged into the ghost rows after them.  The host reads the
+ * all-reduced count of the PREVIOUS round (pinned host copy + event), so the
+ * device always has one round of work queued.  A zero count (no queued tile
+ * and no boundary row changed since the rows every neighbour already merged)
+ * means the global fixed point was reached.
  *
  * This replaces, for a grid too large or too slow for one GPU, the reference's
  * single-threaded propagation loop computeEntireTotalCostMap
@@ -52,7 +54,7 @@ int dymu_dist_destroy(dymu_dist* d);
 /* Sharded solve of the global grid (nx x ny, goal (goal_i, goal_j) in global
  * coordinates); this rank's slab geometry comes from dymu_slab_rows.
  * Collective: every rank calls it with the same nx, ny, goal and
- * passes_per_exchange (0 = 16).  `stream` NULL = the context's stream.
+ * passes_per_exchange (0 = 4).  `stream` NULL = the context's stream.
  * Blocks until converged; stats are this rank's (rounds = exchange rounds). */
 int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t ld, uint32_t nx,
                     uint32_t ny, uint32_t goal_i, uint32_t goal_j, uint32_t passes_per_exchange,

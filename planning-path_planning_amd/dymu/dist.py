@@ -87,7 +87,7 @@ class DistSolver:
             pass
 
     def solve(self, F_slab: int, T_buf: int, ld: int, nx: int, ny: int, goal_i: int,
-              goal_j: int, passes_per_exchange: int = 16, stream: int = 0) -> dict:
+              goal_j: int, passes_per_exchange: int = 0, stream: int = 0) -> dict:
         """F_slab: this rank's rows; T_buf: nrows + 2 rows (ghost, owned..., ghost)."""
         st = DymuStats()
         rc = self._lib.dymu_dist_solve(self.h, F_slab, T_buf, ld, nx, ny, goal_i, goal_j,
@@ -99,7 +99,7 @@ class DistSolver:
 
 
 def vdist_solve(engines, F_slabs, T_bufs, ld: int, nx: int, ny: int, goal_i: int, goal_j: int,
-                passes_per_exchange: int = 16, stream: int = 0) -> list:
+                passes_per_exchange: int = 0, stream: int = 0) -> list:
     """All ranks in one process on one GPU (the C++ loop with copies for RCCL)."""
     lib = load_dist()
     w = len(engines)
