@@ -51,8 +51,8 @@ def parse():
                     help="N>1: 'native' = C++ exchange loop with its own RCCL communicator "
                          "(libdymu_dist); 'python' = dymu.sharded over torch.distributed")
     ap.add_argument("--passes-per-exchange", type=int, default=0,
-                    help="passes per exchange round (0: 4 for the native overlapped loop, "
-                         "16 for the python loop; tools/vdist_rehearsal.py)")
+                    help="passes per exchange round (0: 4 for the native loop, 16 for the "
+                         "python loop; tools/vdist_rehearsal.py)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the row-slab path even at N=1 (exercises the RCCL code path)")
     return ap.parse_args()

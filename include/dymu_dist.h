@@ -5,15 +5,13 @@
  * One process per GPU.  The global ny x nx grid is cut into row slabs
  * (dymu_slab_rows); rank r owns rows [row0, row0+nrows) and solves them with
  * the engine's domain primitives (dymu_dom_*, include/dymu_fim.h).  Every
- * `passes_per_exchange` passes (one round) a rank packs its two boundary rows
- * and sends them to rank-1 / rank+1 (grouped ncclSend/ncclRecv, nx x 8 B per
- * neighbour) together with an all-reduce of its queued-tile count (4 bytes),
- * on a second stream: the transfer overlaps the next round's passes, and the
- * rows are min-merged into the ghost rows after them.  The host reads the
- * all-reduced count of the PREVIOUS round (pinned host copy + event), so the
- * device always has one round of work queued.  A zero count (no queued tile
- * and no boundary row changed since the rows every neighbour already merged)
- * means the global fixed point was reached.
+ * `passes_per_exchange` passes (one round) the ranks swap their boundary rows
+ * with rank-1 / rank+1 (grouped ncclSend/ncclRecv, nx x 8 B per neighbour),
+ * min-merge them into their ghost rows and count the queued tiles in one launch
+ * (dymu_dom_exchange), and all-reduce that count (4 bytes), all on the engine's
+ * stream.  The host reads the all-reduced count of the PREVIOUS round (pinned
+ * host copy + event), so the device always has one round of work queued.  A
+ * zero count means the global fixed point was reached.
  *
  * This replaces, for a grid too large or too slow for one GPU, the reference's
  * single-threaded propagation loop computeEntireTotalCostMap

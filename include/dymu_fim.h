@@ -124,6 +124,11 @@ int dymu_dom_run(dymu_ctx* ctx, uint32_t passes, void* stream);
  * d_pending != NULL also write the number of queued tiles there (int32). */
 int dymu_dom_merge_ghosts(dymu_ctx* ctx, const double* new_lo, const double* new_hi,
                           int32_t* d_pending, void* stream);
+/* dymu_dom_merge_ghosts with the queued-tile count in the SAME launch (the
+ * native sharded loop's per-round step, include/dymu_dist.h): *d_total (device
+ * int32, required) receives the number of tiles queued for the next pass. */
+int dymu_dom_exchange(dymu_ctx* ctx, const double* new_lo, const double* new_hi,
+                      int32_t* d_total, void* stream);
 /* Tiles queued for the next pass (synchronises `stream`). */
 int dymu_dom_pending(dymu_ctx* ctx, void* stream, uint64_t* pending);
 /* End the domain solve; fills stats (passes, visits, sweeps). */

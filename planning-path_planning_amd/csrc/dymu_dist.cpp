@@ -1,16 +1,22 @@
 // dymu_dist.cpp -- row-slab sharded solve driven from C++ (include/dymu_dist.h).
 //
 // The loop the Python SlabSolver (dymu/sharded.py) runs over torch.distributed,
-// here natively, as a two-stream pipeline per round m:
-//   pass stream:  K passes (dymu_dom_run) -> min-merge the rows received in
-//                 round m-1 into the ghost rows (dymu_dom_merge_ghosts, which
-//                 writes the queued-tile count) -> pack this round's boundary
-//                 rows into send buffers (+ a changed-since-last-round flag)
-//   comm stream:  grouped ncclSend/ncclRecv of those rows with rank-1 / rank+1
-//                 and ncclAllReduce of the count -> pinned host copy + event
-// so the xGMI transfer of round m overlaps the passes of round m+1.  The host
-// reads the count of round m-1 after queueing round m and never drains the
-// device queue; one extra round of (empty) passes runs after convergence.
+// here natively, every step on the engine's stream.  Round m:
+//   K passes (dymu_dom_run)
+//   -> grouped ncclSend/ncclRecv: the first / last owned rows straight from T
+//      to rank-1 / rank+1, theirs into two receive rows
+//   -> one exchange launch: min-merge the received rows into the ghost rows and
+//      count the tiles queued for the next pass (dymu_dom_exchange)
+//   -> ncclAllReduce of that count -> 4-byte copy to pinned host memory + event.
+// The host reads the count of round m-1 after queueing round m, so it never
+// drains the device queue; one extra round of (empty) passes runs after
+// convergence.
+//
+// Why one stream and no overlap: the pass kernel is one 1024-thread workgroup
+// per CU at full register use, back to back, so a kernel on a second stream
+// (RCCL's) only gets CUs between passes and the pass stream then waits for it
+// anyway -- measured at N=1: a two-stream pipeline cost ~20 us per round, a
+// CU-masked pass stream (1 CU per XCD left to RCCL) 50% per pass.
 //
 // Reference: the propagation loop this distributes is computeEntireTotalCostMap
 // (src/DyMu_GlobalPathPlanning.cpp:443-468); the per-cell update it converges
@@ -25,17 +31,16 @@
 #include <string>
 #include <vector>
 
-// Exchange buffers of one rank, doubled by round parity so that round m's rows
-// can be in flight while round m+1's passes run: s = rows sent, r = rows
-// received, side 0 = the row shared with rank-1, side 1 = with rank+1.
+// Per-rank exchange buffers: r = the rows received from rank-1 (side 0) and
+// rank+1 (side 1); d_cnt = [queued tiles of this round, its all-reduced value]
+// for two round parities (the host reads round m-1's while round m is queued).
 struct Pipe {
-  double* sbuf = nullptr;   // [2 parity][2 side][cap]
-  double* rbuf = nullptr;   // [2 parity][2 side][cap]
-  int32_t* d_tot = nullptr; // [2 parity] queued tiles + changed-row flag of the round
-  int32_t* d_sum = nullptr; // [2 parity] its all-reduced value
+  double* rbuf = nullptr;    // [2 side][cap]
+  int32_t* d_cnt = nullptr;  // [2 parity][2]
   uint64_t cap = 0;
-  double* s(int par, int side) const { return sbuf + ((uint64_t)par * 2 + side) * cap; }
-  double* r(int par, int side) const { return rbuf + ((uint64_t)par * 2 + side) * cap; }
+  double* r(int side) const { return rbuf + (uint64_t)side * cap; }
+  int32_t* tot(int par) const { return d_cnt + 2 * par; }
+  int32_t* sum(int par) const { return d_cnt + 2 * par + 1; }
 };
 
 struct dymu_dist {
@@ -43,19 +48,19 @@ struct dymu_dist {
   int device = 0;
   int rank = 0, world = 1;
   ncclComm_t comm = nullptr;
-  hipStream_t comm_stream = nullptr;  // RCCL runs here, beside the pass stream
   Pipe pipe;
   int32_t* h_sum = nullptr;  // pinned [2 parity]
-  hipEvent_t ev_pack[2] = {nullptr, nullptr};  // rows of the round packed (pass stream)
-  hipEvent_t ev_comm[2] = {nullptr, nullptr};  // rows received + count reduced (comm stream)
+  hipEvent_t ev[2] = {nullptr, nullptr};
   std::string last_error;
 };
 
 namespace {
 
-// passes per round: the rows of round m are merged after round m+1's passes, so
-// a round must be short (16384^2 rehearsal, 8 virtual ranks: K = 4 -> 1252
-// launches per rank, 8 -> 1472, 16 -> 2400; tools/vdist_rehearsal.py)
+// passes per round: a round costs one RCCL P2P group + one exchange launch + one
+// 4-byte all-reduce on the pass stream (~8 us at N=1 without the P2P), and ghost
+// rows are at most K passes stale.  16384^2 rehearsal (tools/vdist_rehearsal.py,
+// max per-rank pass time): K = 4 -> 37.4 / 27.4 / 21.8 ms at 2 / 4 / 8 ranks in
+// 338 / 327 / 302 rounds; K = 8 -> 44.6 / 32.8 / 27.2 ms in 156 / 163 / 156.
 constexpr uint32_t kDefaultK = 4;
 
 int fail(std::string* err, const char* what, const char* detail, int code) {
@@ -123,75 +128,20 @@ uint64_t max_rounds(uint32_t nx, uint32_t ny, uint32_t K) {
 
 int pipe_alloc(Pipe* p, uint64_t nx) {
   if (p->cap >= nx) return DYMU_OK;
-  if (p->sbuf) (void)hipFree(p->sbuf);
   if (p->rbuf) (void)hipFree(p->rbuf);
-  if (p->d_tot) (void)hipFree(p->d_tot);
+  if (p->d_cnt) (void)hipFree(p->d_cnt);
   *p = Pipe{};
-  if (hipMalloc(&p->sbuf, sizeof(double) * 4 * nx) != hipSuccess ||
-      hipMalloc(&p->rbuf, sizeof(double) * 4 * nx) != hipSuccess ||
-      hipMalloc(&p->d_tot, sizeof(int32_t) * 4) != hipSuccess)
+  if (hipMalloc(&p->rbuf, sizeof(double) * 2 * nx) != hipSuccess ||
+      hipMalloc(&p->d_cnt, sizeof(int32_t) * 4) != hipSuccess)
     return DYMU_ERR_NOMEM;
-  p->d_sum = p->d_tot + 2;
   p->cap = nx;
   return DYMU_OK;
 }
 
 void pipe_free(Pipe* p) {
-  if (p->sbuf) (void)hipFree(p->sbuf);
   if (p->rbuf) (void)hipFree(p->rbuf);
-  if (p->d_tot) (void)hipFree(p->d_tot);
+  if (p->d_cnt) (void)hipFree(p->d_cnt);
   *p = Pipe{};
-}
-
-// Copy the boundary rows into this round's send buffers and add 1 to *tot per
-// wave that saw a cell differ from the previous round's rows (prev NULL: the
-// first round, every finite cell counts).  Values only decrease, so equal rows
-// mean nothing new for the neighbour.
-__global__ void k_pack_rows(const double* row_lo, const double* row_hi, double* s_lo,
-                            double* s_hi, const double* prev_lo, const double* prev_hi,
-                            uint32_t nx, int32_t* tot) {
-  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool ch = false;
-  if (k < nx) {
-    if (row_lo) {
-      const double v = row_lo[k];
-      s_lo[k] = v;
-      ch |= prev_lo ? v != prev_lo[k] : v < __builtin_inf();
-    }
-    if (row_hi) {
-      const double v = row_hi[k];
-      s_hi[k] = v;
-      ch |= prev_hi ? v != prev_hi[k] : v < __builtin_inf();
-    }
-  }
-  if (__any(ch) && (threadIdx.x & 63) == 0) atomicAdd(tot, 1);
-}
-
-hipError_t pack_rows(const Slab& s, const Pipe& p, uint64_t m, hipStream_t st) {
-  const int par = (int)(m & 1);
-  const uint32_t nx = s.dom.nx;
-  if (!s.lo && !s.hi) return hipSuccess;
-  hipLaunchKernelGGL(k_pack_rows, dim3((nx + 255) / 256), dim3(256), 0, st,
-                     s.lo ? s.row(0) : nullptr, s.hi ? s.row(1) : nullptr, p.s(par, 0),
-                     p.s(par, 1), m ? p.s(par ^ 1, 0) : nullptr, m ? p.s(par ^ 1, 1) : nullptr,
-                     nx, p.d_tot + par);
-  return hipGetLastError();
-}
-
-// Round m on the pass stream: K passes, then merge the rows received in round
-// m-1 into the ghost rows (writes the queued-tile count to d_tot[par]), then
-// pack this round's rows (adds the changed-row flag).  The sum over ranks of
-// d_tot[par] is 0 exactly when no rank has queued work and no boundary row
-// changed since the rows every neighbour has already merged: the fixed point.
-int round_compute(dymu_ctx* ctx, const Slab& s, const Pipe& p, uint64_t m, uint32_t K,
-                  hipStream_t st, hipEvent_t rows_in) {
-  const int par = (int)(m & 1);
-  DCALL(dymu_dom_run(ctx, K, st));
-  if (m && rows_in) DHIP(nullptr, hipStreamWaitEvent(st, rows_in, 0));
-  DCALL(dymu_dom_merge_ghosts(ctx, m && s.lo ? p.r(par ^ 1, 0) : nullptr,
-                              m && s.hi ? p.r(par ^ 1, 1) : nullptr, p.d_tot + par, st));
-  DHIP(nullptr, pack_rows(s, p, m, st));
-  return DYMU_OK;
 }
 
 }  // namespace
@@ -221,14 +171,10 @@ int dymu_dist_create(dymu_dist** out, dymu_ctx* ctx, int device,
     return rc;
   };
   if (hipSetDevice(device) != hipSuccess) return bail(DYMU_ERR_HIP);
-  if (hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking) != hipSuccess)
-    return bail(DYMU_ERR_HIP);
   if (hipHostMalloc(&d->h_sum, sizeof(int32_t) * 2, hipHostMallocDefault) != hipSuccess)
     return bail(DYMU_ERR_NOMEM);
-  for (int k = 0; k < 2; ++k)
-    if (hipEventCreateWithFlags(&d->ev_pack[k], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&d->ev_comm[k], hipEventDisableTiming) != hipSuccess)
-      return bail(DYMU_ERR_HIP);
+  for (auto& e : d->ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return bail(DYMU_ERR_HIP);
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof u);
   if (ncclCommInitRank(&d->comm, world, u, rank) != ncclSuccess) {
@@ -242,15 +188,11 @@ int dymu_dist_create(dymu_dist** out, dymu_ctx* ctx, int device,
 int dymu_dist_destroy(dymu_dist* d) {
   if (!d) return DYMU_OK;
   (void)hipSetDevice(d->device);
-  if (d->comm_stream) (void)hipStreamSynchronize(d->comm_stream);
   if (d->comm) (void)ncclCommDestroy(d->comm);
-  for (int k = 0; k < 2; ++k) {
-    if (d->ev_pack[k]) (void)hipEventDestroy(d->ev_pack[k]);
-    if (d->ev_comm[k]) (void)hipEventDestroy(d->ev_comm[k]);
-  }
+  for (auto& e : d->ev)
+    if (e) (void)hipEventDestroy(e);
   pipe_free(&d->pipe);
   if (d->h_sum) (void)hipHostFree(d->h_sum);
-  if (d->comm_stream) (void)hipStreamDestroy(d->comm_stream);
   delete d;
   return DYMU_OK;
 }
@@ -266,50 +208,46 @@ int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t 
   Slab s;
   DCALL(make_slab(F_slab, T_buf, ld, nx, ny, goal_j, d->rank, d->world, &s));
   DHIP(err, hipSetDevice(d->device));
-  if (pipe_alloc(&d->pipe, nx) != DYMU_OK) return fail(err, "pipe_alloc", "out of memory", DYMU_ERR_NOMEM);
+  if (pipe_alloc(&d->pipe, nx) != DYMU_OK)
+    return fail(err, "pipe_alloc", "out of memory", DYMU_ERR_NOMEM);
   const Pipe& p = d->pipe;
-  // the domain primitives and the pass-stream side of the pipeline share one
-  // stream (NULL = the context's); RCCL runs on comm_stream beside it
+  // RCCL and the domain primitives share one stream: NULL = the context's
   if (!stream) stream = dymu_get_stream(d->ctx);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  hipStream_t cs = d->comm_stream;
   DCALL(dymu_dom_begin(d->ctx, &s.dom, s.goal_local >= 0 ? goal_i : 0, s.goal_local, stream));
   const uint64_t cap = max_rounds(nx, ny, K);
   uint64_t m = 0;
   bool done = false;
   for (; !done; ++m) {
     if (m >= cap) {
-      (void)hipStreamSynchronize(cs);
       (void)dymu_dom_finish(d->ctx, stream, nullptr);
       return fail(err, "dymu_dist_solve", "exchange-round cap reached", DYMU_ERR_NOT_CONVERGED);
     }
     const int par = (int)(m & 1);
-    // pass stream: K passes | merge round m-1's rows | pack round m's rows
-    DCALL(round_compute(d->ctx, s, p, m, K, st, d->ev_comm[par ^ 1]));
-    DHIP(err, hipEventRecord(d->ev_pack[par], st));
-    // comm stream: round m's rows to rank-1 / rank+1 and the all-reduced count,
-    // in flight while round m+1's passes run
-    DHIP(err, hipStreamWaitEvent(cs, d->ev_pack[par], 0));
-    DNCCL(err, ncclGroupStart());
-    if (s.lo) {
-      DNCCL(err, ncclSend(p.s(par, 0), nx, ncclDouble, d->rank - 1, d->comm, cs));
-      DNCCL(err, ncclRecv(p.r(par, 0), nx, ncclDouble, d->rank - 1, d->comm, cs));
+    DCALL(dymu_dom_run(d->ctx, K, stream));
+    if (s.lo || s.hi) {
+      DNCCL(err, ncclGroupStart());
+      if (s.lo) {
+        DNCCL(err, ncclSend(s.row(0), nx, ncclDouble, d->rank - 1, d->comm, st));
+        DNCCL(err, ncclRecv(p.r(0), nx, ncclDouble, d->rank - 1, d->comm, st));
+      }
+      if (s.hi) {
+        DNCCL(err, ncclSend(s.row(1), nx, ncclDouble, d->rank + 1, d->comm, st));
+        DNCCL(err, ncclRecv(p.r(1), nx, ncclDouble, d->rank + 1, d->comm, st));
+      }
+      DNCCL(err, ncclGroupEnd());
     }
-    if (s.hi) {
-      DNCCL(err, ncclSend(p.s(par, 1), nx, ncclDouble, d->rank + 1, d->comm, cs));
-      DNCCL(err, ncclRecv(p.r(par, 1), nx, ncclDouble, d->rank + 1, d->comm, cs));
-    }
-    DNCCL(err, ncclAllReduce(p.d_tot + par, p.d_sum + par, 1, ncclInt32, ncclSum, d->comm, cs));
-    DNCCL(err, ncclGroupEnd());
-    DHIP(err, hipMemcpyAsync(d->h_sum + par, p.d_sum + par, sizeof(int32_t),
-                             hipMemcpyDeviceToHost, cs));
-    DHIP(err, hipEventRecord(d->ev_comm[par], cs));
+    DCALL(dymu_dom_exchange(d->ctx, s.lo ? p.r(0) : nullptr, s.hi ? p.r(1) : nullptr, p.tot(par),
+                            stream));
+    DNCCL(err, ncclAllReduce(p.tot(par), p.sum(par), 1, ncclInt32, ncclSum, d->comm, st));
+    DHIP(err, hipMemcpyAsync(d->h_sum + par, p.sum(par), sizeof(int32_t), hipMemcpyDeviceToHost,
+                             st));
+    DHIP(err, hipEventRecord(d->ev[par], st));
     if (m >= 1) {  // round m-1's global count; round m stays queued meanwhile
-      DHIP(err, hipEventSynchronize(d->ev_comm[par ^ 1]));
+      DHIP(err, hipEventSynchronize(d->ev[par ^ 1]));
       done = d->h_sum[par ^ 1] == 0;
     }
   }
-  DHIP(err, hipStreamSynchronize(cs));
   DCALL(dymu_dom_finish(d->ctx, stream, stats));
   if (stats) stats->rounds = m;
   return DYMU_OK;
@@ -353,28 +291,33 @@ int dymu_vdist_solve(dymu_ctx* const* ctxs, int world, const double* const* F_sl
   uint64_t m = 0;
   bool done = false;
   int rc = DYMU_OK;
-  // the schedule of dymu_dist_solve, serialised on one stream: round m's rows
-  // are merged after round m+1's passes
+  // the schedule of dymu_dist_solve with every rank's work serialised on one
+  // stream: device-to-device row copies for RCCL P2P, a host sum for the
+  // all-reduce
   for (; !done && rc == DYMU_OK; ++m) {
     if (m >= cap) {
       rc = DYMU_ERR_NOT_CONVERGED;
       break;
     }
     const int par = (int)(m & 1);
-    for (int r = 0; r < world && rc == DYMU_OK; ++r)
-      rc = round_compute(ctxs[r], s[r], p[r], m, K, st, nullptr);
+    for (int r = 0; r < world && rc == DYMU_OK; ++r) rc = dymu_dom_run(ctxs[r], K, stream);
     if (rc) break;
-    // delivery: rank r's side-0 row -> rank r-1's side-1 receive buffer, and back
-    for (int r = 0; r < world; ++r) {
+    for (int r = 0; r < world; ++r) {  // rank r-1's last row / rank r+1's first row
       if (s[r].lo)
-        DHIP(nullptr, hipMemcpyAsync(p[r].r(par, 0), p[r - 1].s(par, 1), sizeof(double) * nx,
+        DHIP(nullptr, hipMemcpyAsync(p[r].r(0), s[r - 1].row(1), sizeof(double) * nx,
                                      hipMemcpyDeviceToDevice, st));
       if (s[r].hi)
-        DHIP(nullptr, hipMemcpyAsync(p[r].r(par, 1), p[r + 1].s(par, 0), sizeof(double) * nx,
+        DHIP(nullptr, hipMemcpyAsync(p[r].r(1), s[r + 1].row(0), sizeof(double) * nx,
                                      hipMemcpyDeviceToDevice, st));
-      DHIP(nullptr, hipMemcpyAsync(h_tot + par * world + r, p[r].d_tot + par, sizeof(int32_t),
-                                   hipMemcpyDeviceToHost, st));
     }
+    for (int r = 0; r < world && rc == DYMU_OK; ++r) {
+      rc = dymu_dom_exchange(ctxs[r], s[r].lo ? p[r].r(0) : nullptr,
+                             s[r].hi ? p[r].r(1) : nullptr, p[r].tot(par), stream);
+      if (rc == DYMU_OK && hipMemcpyAsync(h_tot + par * world + r, p[r].tot(par), sizeof(int32_t),
+                                          hipMemcpyDeviceToHost, st) != hipSuccess)
+        rc = DYMU_ERR_HIP;
+    }
+    if (rc) break;
     DHIP(nullptr, hipEventRecord(ev[par], st));
     if (m >= 1) {
       DHIP(nullptr, hipEventSynchronize(ev[par ^ 1]));

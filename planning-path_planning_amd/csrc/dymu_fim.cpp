@@ -28,6 +28,7 @@ struct dymu_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   dymu_opts opts{};
   int cu_count = 256;
+  uint32_t* d_xchg = nullptr;  // k_exchange's block ticket (zero between launches)
 
   // 1: 32x32 tile per workgroup, 2: 8x8 tile per wave (Jacobi),
   // 3: two 8x8 tiles per wave (red-black), 4: v3 body + priority passes;
@@ -379,6 +380,23 @@ int dom_merge(dymu_ctx* c, const double* lo, const double* hi, int32_t* d_pendin
   return DYMU_OK;
 }
 
+int dom_exchange(dymu_ctx* c, const double* lo, const double* hi, int32_t* d_total,
+                 hipStream_t st) {
+  auto& D = c->dom;
+  if (!D.live) return DYMU_ERR_STATE;
+  if (!d_total || (lo && !D.a.ghost_lo) || (hi && !D.a.ghost_hi)) return DYMU_ERR_ARG;
+  const uint64_t p = D.p;
+  HIPC(c, launch_exchange(D.a.T, D.a.ld, D.a.nx, D.a.ny, lo, hi, D.a.ntx, D.a.nty,
+                          tile_w(D.variant), D.lists[p % 3], D.counts[p % 3], D.ntiles,
+                          c->d_tile_epoch, D.eb + (uint32_t)p + 1u,
+                          is_prio(D.variant) ? prio_keys(c, p % 3) : nullptr,
+                          is_prio(D.variant) ? prio_hist(c, p % 3) : nullptr,
+                          is_prio(D.variant) ? prio_minkey(c, p % 3) : nullptr,
+                          is_prio(D.variant) ? prio_base(c, p % 3) : nullptr,
+                          is_prio(D.variant) ? prio_delta(c) : nullptr, c->d_xchg, d_total, st));
+  return DYMU_OK;
+}
+
 int dom_finish(dymu_ctx* c, hipStream_t st, dymu_stats* stats, double ms) {
   auto& D = c->dom;
   if (!D.live) return DYMU_ERR_STATE;
@@ -585,6 +603,8 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
   }
   if (e == hipSuccess) e = hipMalloc(&c->d_counts, sizeof(uint32_t) * 4 * kShards);
   if (e == hipSuccess) e = hipMalloc(&c->d_scratch, sizeof(unsigned long long) * 8);
+  if (e == hipSuccess) e = hipMalloc(&c->d_xchg, sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(c->d_xchg, 0, sizeof(uint32_t));
   if (e == hipSuccess)
     e = hipMalloc(&c->d_stats, sizeof(unsigned long long) * kShards * kStatSlots);
   if (e == hipSuccess) e = hipHostMalloc(&c->h_count, sizeof(uint32_t) * 4 * kShards, hipHostMallocDefault);
@@ -612,6 +632,7 @@ int dymu_destroy(dymu_ctx* c) {
   if (c->d_trace) (void)hipFree(c->d_trace);
   if (c->d_lut) (void)hipFree(c->d_lut);
   if (c->d_scratch) (void)hipFree(c->d_scratch);
+  if (c->d_xchg) (void)hipFree(c->d_xchg);
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->d_F) (void)hipFree(c->d_F);
   if (c->d_T) (void)hipFree(c->d_T);
@@ -748,6 +769,13 @@ int dymu_dom_merge_ghosts(dymu_ctx* c, const double* new_lo, const double* new_h
   if (!c) return DYMU_ERR_ARG;
   HIPC(c, hipSetDevice(c->device));
   return dom_merge(c, new_lo, new_hi, d_pending, pick_stream(c, stream));
+}
+
+int dymu_dom_exchange(dymu_ctx* c, const double* new_lo, const double* new_hi,
+                      int32_t* d_total, void* stream) {
+  if (!c) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  return dom_exchange(c, new_lo, new_hi, d_total, pick_stream(c, stream));
 }
 
 int dymu_dom_pending(dymu_ctx* c, void* stream, uint64_t* pending) {

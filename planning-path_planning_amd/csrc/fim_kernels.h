@@ -83,6 +83,12 @@ hipError_t launch_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,
                                uint32_t* tile_epoch, uint32_t epoch, unsigned long long* keys,
                                uint32_t* hist, unsigned long long* minkey, const double* base,
                                const double* delta, hipStream_t st);
+hipError_t launch_exchange(double* T, int64_t ld, int64_t nx, int64_t nrows, const double* new_lo,
+                           const double* new_hi, int ntx, int nty, int tile_w, uint32_t* list,
+                           uint32_t* counts, uint32_t cap, uint32_t* tile_epoch, uint32_t epoch,
+                           unsigned long long* keys, uint32_t* hist, unsigned long long* minkey,
+                           const double* base, const double* delta, uint32_t* ticket,
+                           int32_t* total, hipStream_t st);
 hipError_t launch_eikonal_batch(const double* tx, const double* ty, const double* c, double* out,
                                 uint64_t n, int fast, hipStream_t st);
 hipError_t launch_sum_counts(const uint32_t* counts, int32_t* out, hipStream_t st);

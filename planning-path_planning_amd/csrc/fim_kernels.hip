@@ -1517,48 +1517,89 @@ __global__ void k_prio_seed(unsigned long long* key0, uint32_t* hist0, unsigned 
 // first / last tile row under every column that improved, into the list the
 // next pass reads.  Also used by the single-GPU virtual-slab tests.
 // ---------------------------------------------------------------------------
-__global__ void k_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,
-                               const double* new_lo, const double* new_hi, int ntx, int nty,
-                               int tile_w, uint32_t* list, uint32_t* counts, uint32_t cap,
-                               uint32_t* tile_epoch, uint32_t epoch, unsigned long long* keys,
-                               uint32_t* hist, unsigned long long* minkey, const double* base,
-                               const double* delta) {
-  // blocks of 256 threads start at multiples of 256 columns and tile_w divides
-  // 64, so a tile's columns are tile_w consecutive lanes of one wave.
+struct MergeArgs {
+  double* T;
+  int64_t ld, nx, nrows;
+  int ntx, nty, tile_w;
+  uint32_t* list;
+  uint32_t* counts;
+  uint32_t cap;
+  uint32_t* tile_epoch;
+  uint32_t epoch;
+  unsigned long long* keys;
+  uint32_t* hist;
+  unsigned long long* minkey;
+  const double* base;
+  const double* delta;
+};
+
+// blocks of 256 threads start at multiples of 256 columns and tile_w divides
+// 64, so a tile's columns are tile_w consecutive lanes of one wave.
+__device__ __forceinline__ void merge_rows(const MergeArgs& g, const double* new_lo,
+                                           const double* new_hi) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const uint32_t shard = blockIdx.x % kShards;
-  const unsigned long long tmask = tile_w >= 64 ? ~0ull : ((1ull << tile_w) - 1ull);
+  const unsigned long long tmask = g.tile_w >= 64 ? ~0ull : ((1ull << g.tile_w) - 1ull);
   for (int side = 0; side < 2; ++side) {
     const double* src = side == 0 ? new_lo : new_hi;
     if (!src) continue;  // uniform
     bool seed = false;
     double v = dinf();
-    if (k < nx) {
-      double* g = T + (side == 0 ? -ld : nrows * ld) + k;
+    if (k < g.nx) {
+      double* gh = g.T + (side == 0 ? -g.ld : g.nrows * g.ld) + k;
       v = src[k];
-      if (v < *g) {
-        *g = v;
+      if (v < *gh) {
+        *gh = v;
         seed = true;
       }
     }
     const unsigned long long m = __ballot(seed);
-    const uint32_t tile = (uint32_t)((side == 0 ? 0 : nty - 1) * (int64_t)ntx + k / tile_w);
-    if (keys) {  // v4: key = min improved ghost value under the tile
-      if (seed) atomicMin(&keys[tile], dbits(v));
+    const uint32_t tile = (uint32_t)((side == 0 ? 0 : g.nty - 1) * (int64_t)g.ntx + k / g.tile_w);
+    if (g.keys) {  // v4: key = min improved ghost value under the tile
+      if (seed) atomicMin(&g.keys[tile], dbits(v));
       double wm = seed ? v : dinf();
       for (int o = 32; o > 0; o >>= 1) wm = vmin64(wm, __shfl_xor(wm, o));
-      if (lane == 0 && wm < dinf()) atomicMin(minkey, dbits(wm));
+      if (lane == 0 && wm < dinf()) atomicMin(g.minkey, dbits(wm));
     }
-    if (k < nx && (k % tile_w) == 0 && ((m >> lane) & tmask)) {
-      if (atomicMax(&tile_epoch[tile], epoch) < epoch) {
-        const uint32_t pos = atomicAdd(&counts[shard], 1u);
-        list[(uint64_t)shard * cap + pos] = tile;
-        if (keys) {
-          const double kv = bitsd(keys[tile]);
-          atomicAdd(&hist[shard * kBins + key_bin(kv, *base, 1.0 / *delta)], 1u);
+    if (k < g.nx && (k % g.tile_w) == 0 && ((m >> lane) & tmask)) {
+      if (atomicMax(&g.tile_epoch[tile], g.epoch) < g.epoch) {
+        const uint32_t pos = atomicAdd(&g.counts[shard], 1u);
+        g.list[(uint64_t)shard * g.cap + pos] = tile;
+        if (g.keys) {
+          const double kv = bitsd(g.keys[tile]);
+          atomicAdd(&g.hist[shard * kBins + key_bin(kv, *g.base, 1.0 / *g.delta)], 1u);
         }
       }
+    }
+  }
+}
+
+__global__ void k_merge_ghosts(MergeArgs g, const double* new_lo, const double* new_hi) {
+  merge_rows(g, new_lo, new_hi);
+}
+
+// One launch per round of the native sharded loop (dymu_dist.cpp): merge the
+// received rows, then the last block to finish writes *total = the number of
+// tiles queued for the next pass (k_merge_ghosts + k_sum_counts fused; the
+// per-round launch count is what a short round pays for).  *ticket is reset.
+__global__ void k_exchange(MergeArgs g, const double* new_lo, const double* new_hi,
+                           uint32_t* ticket, int32_t* total) {
+  merge_rows(g, new_lo, new_hi);
+  __shared__ bool s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (s_last && threadIdx.x < 64) {  // every block's list inserts are in
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    uint32_t c = threadIdx.x < kShards ? atomicAdd(&g.counts[threadIdx.x], 0u) : 0u;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (threadIdx.x == 0) {
+      *total = (int32_t)c;
+      atomicExch(ticket, 0u);
     }
   }
 }
@@ -1778,9 +1819,23 @@ hipError_t launch_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,
                                const double* delta, hipStream_t st) {
   const unsigned blocks = (unsigned)((nx + 255) / 256);
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_merge_ghosts, dim3(blocks), dim3(256), 0, st, T, ld, nx, nrows, new_lo,
-                     new_hi, ntx, nty, tile_w, list, counts, cap, tile_epoch, epoch, keys, hist,
-                     minkey, base, delta);
+  const MergeArgs g{T,    ld,    nx,         nrows, ntx,  nty,    tile_w, list,  counts,
+                    cap,  tile_epoch, epoch, keys,  hist, minkey, base,   delta};
+  hipLaunchKernelGGL(k_merge_ghosts, dim3(blocks), dim3(256), 0, st, g, new_lo, new_hi);
+  return hipGetLastError();
+}
+
+hipError_t launch_exchange(double* T, int64_t ld, int64_t nx, int64_t nrows, const double* new_lo,
+                           const double* new_hi, int ntx, int nty, int tile_w, uint32_t* list,
+                           uint32_t* counts, uint32_t cap, uint32_t* tile_epoch, uint32_t epoch,
+                           unsigned long long* keys, uint32_t* hist, unsigned long long* minkey,
+                           const double* base, const double* delta, uint32_t* ticket,
+                           int32_t* total, hipStream_t st) {
+  const unsigned blocks = (unsigned)((nx + 255) / 256);
+  if (blocks == 0) return hipErrorInvalidValue;
+  const MergeArgs g{T,    ld,    nx,         nrows, ntx,  nty,    tile_w, list,  counts,
+                    cap,  tile_epoch, epoch, keys,  hist, minkey, base,   delta};
+  hipLaunchKernelGGL(k_exchange, dim3(blocks), dim3(256), 0, st, g, new_lo, new_hi, ticket, total);
   return hipGetLastError();
 }
 

@@ -115,6 +115,7 @@ FIM_SYMBOLS = {
     "dymu_dom_run": (_i32, [_vp, _u32, _vp]),
     "dymu_dom_merge_ghosts": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dymu_dom_pending": (_i32, [_vp, _vp, ctypes.POINTER(_u64)]),
+    "dymu_dom_exchange": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dymu_dom_finish": (_i32, [_vp, _vp, ctypes.POINTER(DymuStats)]),
     "dymu_last_pass_timing": (_i32, [_vp, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_uint64)]),

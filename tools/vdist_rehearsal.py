@@ -30,9 +30,18 @@ for S in Ss:
     t0 = time.perf_counter()
     st = dist.vdist_solve(engs, dFs, dTs, N, N, N, g[0], g[1], K)
     dt = time.perf_counter() - t0
+    # busy time of each rank's pass launches (events on every launch, a second
+    # solve): the critical path of N real GPUs is about the max over ranks
+    for e in engs:
+        e.set_profiling(1)
+    dist.vdist_solve(engs, dFs, dTs, N, N, N, g[0], g[1], K)
+    busy = [e.last_pass_timing()[0] for e in engs]
+    for e in engs:
+        e.set_profiling(0)
     print(f"S={S} K={K} wall {dt*1e3:.1f} ms  wall/S {dt*1e3/S:.1f} ms  rounds {st[0]['rounds']}  "
           f"passes/rank {[s['passes'] for s in st]}  launches/rank {st[0]['launches']}  "
-          f"visits/rank {[s['tile_visits'] for s in st]}", flush=True)
+          f"visits/rank {[s['tile_visits'] for s in st]}  "
+          f"pass-busy ms/rank {[round(b, 1) for b in busy]}", flush=True)
     for e, dF, dT in zip(engs, dFs, dTs):
         e.free(dF)
         e.free(dT)
