@@ -120,9 +120,10 @@ def test_native_vdist_matches_oracle(dymu, oracle, S, nx, ny, goal, frac, K, kw)
 
 
 def test_native_vdist_large_matches_single(dymu):
-    """2048^2 with the default kernel choice: the stitched slabs equal the
-    single-GPU solve's fixed point (both within ulps of each other)."""
-    N, g = 2048, (700, 1500)
+    """4096^2 in 2 slabs with the default kernel choice (kernel 5 slabs): the
+    stitched slabs equal the single-GPU solve's fixed point (both within ulps
+    of each other)."""
+    N, g = 4096, (700, 1500)
     eng = dymu.Engine()
     dF, dT = eng.alloc(8 * N * N), eng.alloc(8 * N * N)
     eng.synth_speed(dF, N, N, N, 0, 1, 0.02, 3, g[0], g[1])
@@ -134,7 +135,8 @@ def test_native_vdist_large_matches_single(dymu):
     eng.free(dF)
     eng.free(dT)
     eng.close()
-    T, stats = solve_vdist(dymu, F, g, 4, K=16)
+    T, stats = solve_vdist(dymu, F, g, 2, K=4)
+    assert stats[0]["kernel"] == 5
     assert np.array_equal(np.isinf(T), np.isinf(T1))
     fin = np.isfinite(T1)
     assert (np.abs(T[fin] - T1[fin]) / np.maximum(1, T1[fin])).max() <= 1e-12
