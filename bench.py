@@ -15,7 +15,8 @@ N^2 / max-over-ranks solve time.
 Rank 0 prints ONE JSON line with the roofline of the dominant kernel
 (k_fim_pass, per-launch HIP events over the timed region) and the CPU baseline
 (the oracle's heap FMM, same pop order as the reference, one thread, on a
-bounded sample).
+bounded sample), plus `cpu_reference_algorithm`: the reference's own
+linear-scan narrow band (SURVEY s8(d) cpu_fmm_linear) on a 1024^2 sample.
 """
 import argparse
 import json
@@ -77,6 +78,31 @@ def cpu_baseline(n_edge, obst):
         "sample": f"{n_edge}x{n_edge} config-3 grid (2% obstacles, goal centre), oracle heap "
                   f"FMM with the reference's pop order, 1 thread, {dt:.1f}s; "
                   f"host {platform.processor() or platform.machine()}",
+    }
+
+
+def cpu_reference_algorithm(n_edge, obst):
+    """SURVEY s8(d) cpu_fmm_linear: the oracle's restatement of the reference's own
+    narrow band (minCostGlobalNode, src/DyMu_GlobalPathPlanning.cpp:551-568: linear
+    scan for the first strict minimum + vector::erase), 1 thread, bounded sample.
+    Its cost is O(cells x band), so the rate falls as the grid grows."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi
+
+    o = oracle_ffi.load()
+    g = (n_edge // 2, n_edge // 2)
+    F = o.synth_speed(n_edge, n_edge, seed=1, obst_frac=obst, obst_seed=3, goal=g)
+    t0 = time.perf_counter()
+    o.fmm(F, g, linear=True)
+    dt = time.perf_counter() - t0
+    return {
+        "value": n_edge * n_edge / dt / 1e6,
+        "unit": "Mcells/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{n_edge}x{n_edge} config-3 grid, oracle FMM with the reference's linear-scan "
+                  f"narrow band (:551-568), 1 thread, {dt:.1f}s; the rate falls with grid size "
+                  f"(O(cells x band))",
     }
 
 
@@ -216,6 +242,7 @@ def main():
     }
     if world == 1 and args.cpu_sample > 0:
         line["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.obst)
+        line["cpu_reference_algorithm"] = cpu_reference_algorithm(1024, args.obst)
     print(json.dumps(line), flush=True)
 
 
