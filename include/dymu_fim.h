@@ -19,7 +19,8 @@
  * and +inf (or NaN) for an obstacle.  F must be >= 0 or +inf.  T[k] receives
  * the converged total cost; +inf marks unreachable cells and obstacles; the
  * goal holds 0.  Results equal the reference FMM within |dT| <= 1e-12*max(1,T)
- * with an identical +inf mask.
+ * with an identical +inf mask for speeds with 2*F*F finite
+ * (F < 1.34e154); beyond that the reference update itself is order-dependent.
  *
  * All functions return DYMU_OK (0) or a negative dymu_status.  Contexts are
  * not thread-safe; use one context per host thread.
