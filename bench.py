@@ -33,6 +33,13 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
 BYTES_PER_CELL_VISIT = 24  # read T 8 + read F 8 + write T 8
 BYTES_PER_CELL_SOLVE = 16  # read F once + write T once
+# The pass kernel's real limiter is the fp64 VALU (and the latency of its pass chain,
+# DESIGN.md s4), not HBM.  Kernel 5's sweep loop issues 201 VALU instructions per pair
+# of sweeps over a lane's 4 cells (ISA count of the fast path, llvm -S of
+# fim_kernels.hip): 25.1 per cell update.  Peak: MI355X fp64 vector 78.6 TFLOP/s =
+# 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz = 39.3 T lane-instructions/s.
+VALU_PER_CELL_UPDATE = {5: 201 / 8}
+VALU_PEAK_T = 256 * 4 * 16 * 2.4e9 / 1e12
 
 
 def parse():
@@ -198,6 +205,18 @@ def main():
             },
             "headline_solve_GBs": round(N * N * BYTES_PER_CELL_SOLVE * K / dt / 1e9, 3),
         }
+        vpu = VALU_PER_CELL_UPDATE.get(st.get("kernel"))
+        if vpu:
+            sweeps = tot.get("rank0_inner_sweeps", tot["inner_sweeps"])
+            ops = sweeps * st["tile_w"] * st["tile_h"] * vpu / tot["launches"]
+            roof["valu"] = {
+                "per_unit": f"{vpu:.1f} fp64-VALU instructions per cell update x tile cells x "
+                            "in-tile sweeps in the launch",
+                "achieved": round(ops / launch_s / 1e12, 3),
+                "peak": VALU_PEAK_T,
+                "unit": "T lane-instr/s",
+                "frac": round(ops / launch_s / 1e12 / VALU_PEAK_T, 4),
+            }
     if roof is not None:
         # HBM bytes per launch from the PMC counters of the same kernel and
         # workload (tools/pmc_round.sh -> tools/pmc_summary.py), if committed

@@ -96,6 +96,7 @@ def run(args):
         print(f"rank {rank}: rows {row0}+{nrows} {tot} {time.perf_counter() - t0:.4f}s",
               flush=True)
     tot["rank0_tile_visits"] = tot["tile_visits"]  # this rank's (rank 0 reports)
+    tot["rank0_inner_sweeps"] = tot["inner_sweeps"]
     agg = torch.tensor([tot["tile_visits"], tot["inner_sweeps"], tot["passes"]],
                        dtype=torch.float64, device=dt.device)
     dist.all_reduce(agg)
