@@ -241,14 +241,18 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   a.nty = (int)nty;
   a.ghost_lo = ghost_lo;
   a.ghost_hi = ghost_hi;
-  // v5: a short sweep cap bounds the pass latency (capped tiles re-queue themselves);
-  // from 2^20 tiles (16384^2) the pass tail outweighs the extra passes of a 12 cap
-  // (measured: 12 is 3% faster at 16384^2, 8% slower at 4096^2)
-  const int v5_inner = ntiles >= (1u << 20) ? 12 : 16;
+  // v5: a sweep cap of 16 bounds the visit (capped tiles re-queue themselves); from
+  // 2^20 tiles (16384^2) a pass is ended by the capped visits of the busiest SIMDs,
+  // so there a visit also stops sweeping 14 us into the pass (re-queued like a capped
+  // one): 46.0 vs 49.2 ms at 16384^2; at 4096^2 it costs 2%
+  const bool big = ntiles >= (1u << 20);
   a.max_inner = c->opts.max_inner > 0 ? c->opts.max_inner
-                : variant == 5            ? v5_inner
+                : variant == 5            ? 16
                                           : 4 * (TWd + THd);
   if (const char* kv = std::getenv("DYMU_MAX_INNER")) a.max_inner = std::max(1, std::atoi(kv));
+  a.sweep_deadline = (variant == 5 && big) ? 1400u : 0u;  // 10-ns s_memrealtime ticks
+  if (const char* kv = std::getenv("DYMU_SWEEP_DEADLINE"))
+    a.sweep_deadline = (uint32_t)std::max(0, std::atoi(kv));
   a.shard_cap = ntiles;
   a.tile_epoch = c->d_tile_epoch;
   a.stats = c->d_stats;

@@ -53,6 +53,8 @@ struct PassArgs {
   float target_frac;      // ... at least this fraction of the active list
   int prune;              // activate a neighbour only through edge cells below its halo value
   unsigned long long* trace;  // debug: kTracePts s_memrealtime stamps per block, or null
+  uint32_t sweep_deadline;  // kernel 5 (dyn): > 0: a visit stops sweeping this many 10-ns ticks
+                            // after its workgroup started the pass (re-queued as if capped)
 };
 
 constexpr int kBins = 64;  // v4/v5 key histogram bins

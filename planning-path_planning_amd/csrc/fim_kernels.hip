@@ -916,10 +916,12 @@ template <bool FAST>
 __device__ __forceinline__ int rb_sweeps4(double* img, const int (&sr)[2], const int (&sb)[2],
                                           const double (&fr)[2], const double (&fb)[2],
                                           double (&tr)[2], double (&tb)[2], int max_inner,
-                                          bool& capped) {
+                                          bool& capped, unsigned long long stop_at = ~0ull) {
   int sweeps = 0;
   capped = true;
-  while (sweeps < max_inner) {
+  // past stop_at (the pass deadline) a visit ends as if capped -- but only after
+  // its first sweep pair, so every visit makes progress and the solve terminates
+  while (sweeps < max_inner && (sweeps == 0 || __builtin_amdgcn_s_memrealtime() < stop_at)) {
     bool i0, i1, i2, i3;
 #if DYMU_CHECK2
     // two sweeps per convergence test: the second sweep's flags decide (a sweep
@@ -961,7 +963,7 @@ struct NoGate {
 template <class Gate = NoGate>
 __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned long long* ek,
                                        bool has, int tx, int ty, int lane, bool& capped,
-                                       Gate gate = Gate()) {
+                                       Gate gate = Gate(), unsigned long long stop_at = ~0ull) {
   constexpr int TT = 16;
   const int r = lane >> 2, q = lane & 3, odd = r & 1;
   const int cr[2] = {4 * q + odd, 4 * q + 2 + odd};
@@ -1025,8 +1027,8 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
   const bool fast = __all(!(fr[0] < kFastMinF) && !(fr[1] < kFastMinF) &&
                           !(fb[0] < kFastMinF) && !(fb[1] < kFastMinF));
   const int sweeps =
-      fast ? rb_sweeps4<true>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped)
-           : rb_sweeps4<false>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped);
+      fast ? rb_sweeps4<true>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped, stop_at)
+           : rb_sweeps4<false>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped, stop_at);
   unsigned long long v[4];  // cells 4q..4q+3 in column order, decreased value or +inf
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -1302,7 +1304,9 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   const int wv = tid >> 6;
   const uint32_t shard = blockIdx.x % kShards;
   unsigned long long* trace = a.trace ? a.trace + (uint64_t)blockIdx.x * kTracePts : nullptr;
-  if (trace && tid == 0) trace[0] = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long stop_at = a.sweep_deadline ? t_start + a.sweep_deadline : ~0ull;
+  if (trace && tid == 0) trace[0] = t_start;
 
   const double delta = *a.delta;
   const double origin_in = *a.base_in;
@@ -1389,9 +1393,9 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     if (lane < 4) ek[lane] = kInfBits;
     if (trace && tid == 0 && first) trace[6] = __builtin_amdgcn_s_memrealtime();
     bool capped = false;
-    const int sweeps = visit16(a, img, ek, true, tx, ty, lane, capped, [&] {
-      return key_bin(bitsd(kb), origin_in, inv_delta) <= bstar;
-    });
+    const int sweeps = visit16(
+        a, img, ek, true, tx, ty, lane, capped,
+        [&] { return key_bin(bitsd(kb), origin_in, inv_delta) <= bstar; }, stop_at);
     if (lane == 0) a.key_in[tile] = kInfBits;
     if (sweeps < 0) {  // deferred to the next pass with its key
       if (lane == 0) enqueue(tile, kb);
