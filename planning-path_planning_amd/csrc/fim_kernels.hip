@@ -252,6 +252,17 @@ __device__ __forceinline__ uint32_t list_at(const uint32_t* list, uint32_t cap,
   return list[(uint64_t)k * cap + (li - pref[k])];
 }
 
+// list_at for a wave-uniform li: lane q reads pref[q], one ballot counts the
+// shards that start at or before li (one LDS read and a few VALU ops instead of
+// fifteen reads and a 64-bit add chain)
+__device__ __forceinline__ uint32_t list_at_wave(const uint32_t* list, uint32_t cap,
+                                                 const uint32_t* pref, uint32_t li, int lane) {
+  const uint32_t p = lane < kShards ? pref[lane] : 0u;
+  const int k = __popcll(__ballot(lane >= 1 && lane < kShards && li >= p));
+  const uint32_t base = __builtin_amdgcn_readlane(p, k);
+  return list[(uint64_t)k * cap + (li - base)];
+}
+
 __global__ __launch_bounds__(256) void k_fim_pass_w8(PassArgs a) {
   __shared__ uint32_t s_q[QCAP];
   __shared__ uint32_t s_pref[kShards + 1];
@@ -975,37 +986,66 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
   const int64_t gj = j0 + r;
   const bool rowin = has && gj < a.ny;
   double tr[2], tb[2], fr[2], fb[2];
+  double hw, he, hs[4], hn[4];
+  // interior tile (wave-uniform): every cell and halo address is valid, so every
+  // lane loads unmasked -- no +inf defaults, bounds tests or exec-mask branches.
+  // The halo loads of lanes that do not own a halo cell read valid duplicates
+  // of their neighbours' addresses and are never stored to the image.
+  const bool interior = has && i0 > 0 && i0 + TT < a.nx && (j0 > 0 || a.ghost_lo) &&
+                        (j0 + TT < a.ny || (j0 + TT == a.ny && a.ghost_hi));
+  if (interior) {
+    const double* Tr = a.T + gj * a.ld + i0;
+    const double* Fr = a.F + gj * a.ld + i0;
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    tr[k] = fr[k] = tb[k] = fb[k] = dinf();
-    if (rowin && i0 + cr[k] < a.nx) {
-      tr[k] = a.T[gj * a.ld + i0 + cr[k]];
-      fr[k] = a.F[gj * a.ld + i0 + cr[k]];
+    for (int k = 0; k < 2; ++k) {
+      tr[k] = Tr[cr[k]];
+      fr[k] = Fr[cr[k]];
+      tb[k] = Tr[cb[k]];
+      fb[k] = Fr[cb[k]];
     }
-    if (rowin && i0 + cb[k] < a.nx) {
-      tb[k] = a.T[gj * a.ld + i0 + cb[k]];
-      fb[k] = a.F[gj * a.ld + i0 + cb[k]];
-    }
-  }
-  double hw = dinf(), he = dinf(), hs[4], hn[4];
-  if (rowin) {
-    if (q == 0 && i0 > 0) hw = a.T[gj * a.ld + (i0 - 1)];
-    if (q == 3 && i0 + TT < a.nx) he = a.T[gj * a.ld + (i0 + TT)];
-  }
+    hw = Tr[-1];
+    he = Tr[TT];
+    const double* Ts = a.T + (j0 - 1) * a.ld + i0 + 4 * q;
+    const double* Tn = a.T + (j0 + TT) * a.ld + i0 + 4 * q;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) hs[k] = hn[k] = dinf();
-  if (has) {
-    if (r == 0 && (j0 > 0 || a.ghost_lo)) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (i0 + 4 * q + k < a.nx) hs[k] = a.T[(j0 - 1) * a.ld + i0 + 4 * q + k];
+    for (int k = 0; k < 4; ++k) {
+      hs[k] = Ts[k];
+      hn[k] = Tn[k];
     }
-    if (r == TT - 1) {
-      const int64_t jn = j0 + TT;
-      if (jn < a.ny || (jn == a.ny && a.ghost_hi)) {
+  } else {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      tr[k] = fr[k] = tb[k] = fb[k] = dinf();
+      if (rowin && i0 + cr[k] < a.nx) {
+        tr[k] = a.T[gj * a.ld + i0 + cr[k]];
+        fr[k] = a.F[gj * a.ld + i0 + cr[k]];
+      }
+      if (rowin && i0 + cb[k] < a.nx) {
+        tb[k] = a.T[gj * a.ld + i0 + cb[k]];
+        fb[k] = a.F[gj * a.ld + i0 + cb[k]];
+      }
+    }
+    hw = dinf();
+    he = dinf();
+    if (rowin) {
+      if (q == 0 && i0 > 0) hw = a.T[gj * a.ld + (i0 - 1)];
+      if (q == 3 && i0 + TT < a.nx) he = a.T[gj * a.ld + (i0 + TT)];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) hs[k] = hn[k] = dinf();
+    if (has) {
+      if (r == 0 && (j0 > 0 || a.ghost_lo)) {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          if (i0 + 4 * q + k < a.nx) hn[k] = a.T[jn * a.ld + i0 + 4 * q + k];
+          if (i0 + 4 * q + k < a.nx) hs[k] = a.T[(j0 - 1) * a.ld + i0 + 4 * q + k];
+      }
+      if (r == TT - 1) {
+        const int64_t jn = j0 + TT;
+        if (jn < a.ny || (jn == a.ny && a.ghost_hi)) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (i0 + 4 * q + k < a.nx) hn[k] = a.T[jn * a.ld + i0 + 4 * q + k];
+        }
       }
     }
   }
@@ -1030,13 +1070,21 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
       fast ? rb_sweeps4<true>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped, stop_at)
            : rb_sweeps4<false>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped, stop_at);
   unsigned long long v[4];  // cells 4q..4q+3 in column order, decreased value or +inf
+  {
+    unsigned long long vr[2], vb[2];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const bool dr = tr[k] < tr0[k], db = tb[k] < tb0[k];
-    if (dr) a.T[gj * a.ld + i0 + cr[k]] = tr[k];
-    if (db) a.T[gj * a.ld + i0 + cb[k]] = tb[k];
-    v[cr[k] - 4 * q] = dr ? dbits(tr[k]) : kInfBits;
-    v[cb[k] - 4 * q] = db ? dbits(tb[k]) : kInfBits;
+    for (int k = 0; k < 2; ++k) {
+      const bool dr = tr[k] < tr0[k], db = tb[k] < tb0[k];
+      if (dr) a.T[gj * a.ld + i0 + cr[k]] = tr[k];
+      if (db) a.T[gj * a.ld + i0 + cb[k]] = tb[k];
+      vr[k] = dr ? dbits(tr[k]) : kInfBits;
+      vb[k] = db ? dbits(tb[k]) : kInfBits;
+    }
+    // red columns 4q+odd, 4q+2+odd; black the other two (no runtime-indexed store)
+    v[0] = odd ? vb[0] : vr[0];
+    v[1] = odd ? vr[0] : vb[0];
+    v[2] = odd ? vb[1] : vr[1];
+    v[3] = odd ? vr[1] : vb[1];
   }
   // prune as in visit8, halo re-read from the image
   auto across = [&](unsigned long long vv, double hx) {
@@ -1386,7 +1434,8 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     if (lane == 0) e = c0 + atomicAdd(&s_next, 1u);
     e = __builtin_amdgcn_readfirstlane(e);
     if (e >= c1) break;
-    const uint32_t tile = __builtin_amdgcn_readfirstlane(list_at(a.list_in, a.shard_cap, s_pref, e));
+    const uint32_t tile =
+        __builtin_amdgcn_readfirstlane(list_at_wave(a.list_in, a.shard_cap, s_pref, e, lane));
     const unsigned long long kb = a.key_in[tile];
     const int tx = (int)(tile % (uint32_t)a.ntx);
     const int ty = (int)(tile / (uint32_t)a.ntx);
