@@ -1069,51 +1069,31 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
   const int sweeps =
       fast ? rb_sweeps4<true>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped, stop_at)
            : rb_sweeps4<false>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped, stop_at);
-  unsigned long long v[4];  // cells 4q..4q+3 in column order, decreased value or +inf
-  {
-    unsigned long long vr[2], vb[2];
+  // write back decreased cells; dr/db: the decreased value or +inf.  Keys are
+  // non-negative doubles, so the u64 order of their bits (ek) is their f64
+  // order and the edge minima below are v_min_f64 / v_cmp_f64 work.
+  double dr[2], db[2];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const bool dr = tr[k] < tr0[k], db = tb[k] < tb0[k];
-      if (dr) a.T[gj * a.ld + i0 + cr[k]] = tr[k];
-      if (db) a.T[gj * a.ld + i0 + cb[k]] = tb[k];
-      vr[k] = dr ? dbits(tr[k]) : kInfBits;
-      vb[k] = db ? dbits(tb[k]) : kInfBits;
-    }
-    // red columns 4q+odd, 4q+2+odd; black the other two (no runtime-indexed store)
-    v[0] = odd ? vb[0] : vr[0];
-    v[1] = odd ? vr[0] : vb[0];
-    v[2] = odd ? vb[1] : vr[1];
-    v[3] = odd ? vr[1] : vb[1];
+  for (int k = 0; k < 2; ++k) {
+    const bool cr_ = tr[k] < tr0[k], cb_ = tb[k] < tb0[k];
+    if (cr_) a.T[gj * a.ld + i0 + cr[k]] = tr[k];
+    if (cb_) a.T[gj * a.ld + i0 + cb[k]] = tb[k];
+    dr[k] = cr_ ? tr[k] : dinf();
+    db[k] = cb_ ? tb[k] : dinf();
   }
-  // prune as in visit8, halo re-read from the image
-  auto across = [&](unsigned long long vv, double hx) {
-    return (vv != kInfBits && (!a.prune || vv < dbits(hx))) ? vv : kInfBits;
-  };
-  auto min4 = [&](const double* h) {
-    unsigned long long m = kInfBits;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const unsigned long long x = across(v[k], h[k]);
-      m = x < m ? x : m;
-    }
-    return m;
-  };
-  if (r == 0) {
-    const unsigned long long m = min4(img + 1 + 4 * q);
-    if (m != kInfBits) atomicMin(&ek[0], m);
+  // exact pruning (as visit8): a decreased edge cell counts only if it is below
+  // the halo snapshot across the edge, re-read from the image
+  auto across = [&](double v, double hx) { return (!a.prune || v < hx) ? v : dinf(); };
+  if (r == 0 || r == TT - 1) {  // S / N edge: rows 0 and 15 (disjoint lanes), halo row beyond
+    const int vo = r == 0 ? -IP16 : IP16;
+    const double m = vmin64(vmin64(across(dr[0], img[sr[0] + vo]), across(dr[1], img[sr[1] + vo])),
+                            vmin64(across(db[0], img[sb[0] + vo]), across(db[1], img[sb[1] + vo])));
+    if (m < dinf()) atomicMin(&ek[r == 0 ? 0 : 3], dbits(m));
   }
-  if (r == TT - 1) {
-    const unsigned long long m = min4(img + (TT + 1) * IP16 + 1 + 4 * q);
-    if (m != kInfBits) atomicMin(&ek[3], m);
-  }
-  if (q == 0) {
-    const unsigned long long m = across(v[0], img[row]);
-    if (m != kInfBits) atomicMin(&ek[1], m);
-  }
-  if (q == 3) {
-    const unsigned long long m = across(v[3], img[row + TT + 1]);
-    if (m != kInfBits) atomicMin(&ek[2], m);
+  if (q == 0 || q == 3) {  // W / E edge: column 0 (cr[0] or cb[0]) / column 15 (cr[1] or cb[1])
+    const double c = q == 0 ? (odd ? db[0] : dr[0]) : (odd ? dr[1] : db[1]);
+    const double m = across(c, img[q == 0 ? row : row + TT + 1]);
+    if (m < dinf()) atomicMin(&ek[q == 0 ? 1 : 2], dbits(m));
   }
   return sweeps;
 }
