@@ -221,7 +221,12 @@ def main():
         # HBM bytes per launch from the PMC counters of the same kernel and
         # workload (tools/pmc_round.sh -> tools/pmc_summary.py), if committed
         import glob
-        pm = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+        import re
+
+        def natural(f):  # pmc_r01_v10 after pmc_r01_v9
+            return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", f)]
+
+        pm = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")), key=natural)
         for f in reversed(pm):  # newest summary of THIS kernel
             d = json.load(open(f))
             if d.get("kernel") and roof["kernel"] in d["kernel"] and d.get("grid", N) == N:
