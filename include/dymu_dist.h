@@ -8,10 +8,11 @@
  * `passes_per_exchange` passes (one round) the ranks swap their boundary rows
  * with rank-1 / rank+1 (grouped ncclSend/ncclRecv, nx x 8 B per neighbour),
  * min-merge them into their ghost rows and count the queued tiles in one launch
- * (dymu_dom_exchange), and all-reduce that count (4 bytes), all on the engine's
- * stream.  The host reads the all-reduced count of the PREVIOUS round (pinned
- * host copy + event), so the device always has one round of work queued.  A
- * zero count means the global fixed point was reached.
+ * (dymu_dom_exchange), and on every 4th round all-reduce that count (4 bytes),
+ * all on the engine's stream.  The host reads the all-reduced count of the
+ * PREVIOUS check (pinned host copy + event), so the device always has work
+ * queued.  A zero count after a round means the global fixed point was reached
+ * (DESIGN.md s5).
  *
  * This replaces, for a grid too large or too slow for one GPU, the reference's
  * single-threaded propagation loop computeEntireTotalCostMap

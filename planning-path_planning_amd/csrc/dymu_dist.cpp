@@ -7,10 +7,11 @@
 //      to rank-1 / rank+1, theirs into two receive rows
 //   -> one exchange launch: min-merge the received rows into the ghost rows and
 //      count the tiles queued for the next pass (dymu_dom_exchange)
-//   -> ncclAllReduce of that count -> 4-byte copy to pinned host memory + event.
-// The host reads the count of round m-1 after queueing round m, so it never
-// drains the device queue; one extra round of (empty) passes runs after
-// convergence.
+//   -> every kCheckEvery-th round: ncclAllReduce of that count -> 4-byte copy to
+//      pinned host memory + event.
+// The host reads the previous check's count after queueing the current one, so
+// it never drains the device queue; up to two check intervals of (empty) rounds
+// run after convergence.
 //
 // Why one stream and no overlap: the pass kernel is one 1024-thread workgroup
 // per CU at full register use, back to back, so a kernel on a second stream
@@ -62,6 +63,12 @@ namespace {
 // max per-rank pass time): K = 4 -> 37.4 / 27.4 / 21.8 ms at 2 / 4 / 8 ranks in
 // 338 / 327 / 302 rounds; K = 8 -> 44.6 / 32.8 / 27.2 ms in 156 / 163 / 156.
 constexpr uint32_t kDefaultK = 4;
+// rounds per termination check: the 4-byte all-reduce (and its copy to the host)
+// sits on the pass stream, so it runs on every kCheckEvery-th round only.  A zero
+// global count after ANY round is the fixed point (no rank has work and no ghost
+// improved), so checking a subset of rounds is exact; the solve ends at most two
+// check intervals of empty rounds later.
+constexpr uint64_t kCheckEvery = 4;
 
 int fail(std::string* err, const char* what, const char* detail, int code) {
   if (err) {
@@ -215,15 +222,16 @@ int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t 
   if (!stream) stream = dymu_get_stream(d->ctx);
   hipStream_t st = static_cast<hipStream_t>(stream);
   DCALL(dymu_dom_begin(d->ctx, &s.dom, s.goal_local >= 0 ? goal_i : 0, s.goal_local, stream));
-  const uint64_t cap = max_rounds(nx, ny, K);
-  uint64_t m = 0;
+  const uint64_t cap = max_rounds(nx, ny, K) + 2 * kCheckEvery;
+  uint64_t m = 0, checks = 0;
   bool done = false;
   for (; !done; ++m) {
     if (m >= cap) {
       (void)dymu_dom_finish(d->ctx, stream, nullptr);
       return fail(err, "dymu_dist_solve", "exchange-round cap reached", DYMU_ERR_NOT_CONVERGED);
     }
-    const int par = (int)(m & 1);
+    const bool check = (m % kCheckEvery) == kCheckEvery - 1;
+    const int par = (int)(checks & 1);
     DCALL(dymu_dom_run(d->ctx, K, stream));
     if (s.lo || s.hi) {
       DNCCL(err, ncclGroupStart());
@@ -239,14 +247,16 @@ int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t 
     }
     DCALL(dymu_dom_exchange(d->ctx, s.lo ? p.r(0) : nullptr, s.hi ? p.r(1) : nullptr, p.tot(par),
                             stream));
+    if (!check) continue;
     DNCCL(err, ncclAllReduce(p.tot(par), p.sum(par), 1, ncclInt32, ncclSum, d->comm, st));
     DHIP(err, hipMemcpyAsync(d->h_sum + par, p.sum(par), sizeof(int32_t), hipMemcpyDeviceToHost,
                              st));
     DHIP(err, hipEventRecord(d->ev[par], st));
-    if (m >= 1) {  // round m-1's global count; round m stays queued meanwhile
+    if (checks >= 1) {  // the previous check's global count; this one stays queued meanwhile
       DHIP(err, hipEventSynchronize(d->ev[par ^ 1]));
       done = d->h_sum[par ^ 1] == 0;
     }
+    ++checks;
   }
   DCALL(dymu_dom_finish(d->ctx, stream, stats));
   if (stats) stats->rounds = m;
@@ -287,8 +297,8 @@ int dymu_vdist_solve(dymu_ctx* const* ctxs, int world, const double* const* F_sl
   for (int r = 0; r < world; ++r)
     DCALL(dymu_dom_begin(ctxs[r], &s[r].dom, s[r].goal_local >= 0 ? goal_i : 0, s[r].goal_local,
                          stream));
-  const uint64_t cap = max_rounds(nx, ny, K);
-  uint64_t m = 0;
+  const uint64_t cap = max_rounds(nx, ny, K) + 2 * kCheckEvery;
+  uint64_t m = 0, checks = 0;
   bool done = false;
   int rc = DYMU_OK;
   // the schedule of dymu_dist_solve with every rank's work serialised on one
@@ -299,7 +309,8 @@ int dymu_vdist_solve(dymu_ctx* const* ctxs, int world, const double* const* F_sl
       rc = DYMU_ERR_NOT_CONVERGED;
       break;
     }
-    const int par = (int)(m & 1);
+    const bool check = (m % kCheckEvery) == kCheckEvery - 1;
+    const int par = (int)(checks & 1);
     for (int r = 0; r < world && rc == DYMU_OK; ++r) rc = dymu_dom_run(ctxs[r], K, stream);
     if (rc) break;
     for (int r = 0; r < world; ++r) {  // rank r-1's last row / rank r+1's first row
@@ -313,18 +324,21 @@ int dymu_vdist_solve(dymu_ctx* const* ctxs, int world, const double* const* F_sl
     for (int r = 0; r < world && rc == DYMU_OK; ++r) {
       rc = dymu_dom_exchange(ctxs[r], s[r].lo ? p[r].r(0) : nullptr,
                              s[r].hi ? p[r].r(1) : nullptr, p[r].tot(par), stream);
-      if (rc == DYMU_OK && hipMemcpyAsync(h_tot + par * world + r, p[r].tot(par), sizeof(int32_t),
-                                          hipMemcpyDeviceToHost, st) != hipSuccess)
+      if (rc == DYMU_OK && check &&
+          hipMemcpyAsync(h_tot + par * world + r, p[r].tot(par), sizeof(int32_t),
+                         hipMemcpyDeviceToHost, st) != hipSuccess)
         rc = DYMU_ERR_HIP;
     }
     if (rc) break;
+    if (!check) continue;
     DHIP(nullptr, hipEventRecord(ev[par], st));
-    if (m >= 1) {
+    if (checks >= 1) {
       DHIP(nullptr, hipEventSynchronize(ev[par ^ 1]));
       int64_t tot = 0;
       for (int r = 0; r < world; ++r) tot += h_tot[(par ^ 1) * world + r];
       done = tot == 0;
     }
+    ++checks;
   }
   for (int r = 0; r < world; ++r) {
     dymu_stats tmp;
