@@ -126,7 +126,7 @@ class DyMuPathPlanner {
   double goal_heading_ = 0.0;
 
   dymu_ctx* ctx_ = nullptr;
-  dymu_opts opts_{-1, 0, 0, 0, 0, 0, 0};
+  dymu_opts opts_{-1, 0, 0, 0, 0, 0, 0, 0};
   dymu_stats stats_{};
   std::vector<double> speed_;   // F of the last solve
   std::vector<double> packed_;  // F being packed

@@ -61,6 +61,10 @@ typedef struct dymu_opts {
                            passes on 16x16 tiles */
   int prio_target;      /* kernels 4/5: tiles relaxed per pass; 0 = default
                            (64 per CU for 4, 8 per CU for 5) */
+  int exact_sqrt;       /* kernel 5: 1 = correctly rounded sqrt in the sweeps (every update
+                           bit-identical to the reference formula); 0 = default: one
+                           Goldschmidt step, <= 36 ulp on the sqrt term, solve error vs the
+                           reference FMM unchanged (<= 6e-15 rel) */
 } dymu_opts;
 
 typedef struct dymu_stats {
@@ -146,7 +150,8 @@ int dymu_synth_speed(dymu_ctx* ctx, double* dF, uint32_t nx, uint32_t ny, uint64
 
 /* Arithmetic self-test: out[k] = the kernels' Eikonal candidate for
  * (Tx[k], Ty[k], C[k]) (reference :531-535), computed by the same device code
- * the pass kernels use (fast = 1: the range-restricted correctly rounded sqrt).
+ * the pass kernels use (fast = 1: the range-restricted correctly rounded sqrt;
+ * fast = 2: kernel 5's default sweep sqrt, one Goldschmidt step).
  * Device pointers; blocks until done. */
 int dymu_eikonal_batch(dymu_ctx* ctx, const double* tx, const double* ty, const double* c,
                        double* out, uint64_t n, int fast);

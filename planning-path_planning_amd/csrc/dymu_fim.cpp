@@ -253,6 +253,8 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   a.sweep_deadline = (variant == 5 && big) ? 1400u : 0u;  // 10-ns s_memrealtime ticks
   if (const char* kv = std::getenv("DYMU_SWEEP_DEADLINE"))
     a.sweep_deadline = (uint32_t)std::max(0, std::atoi(kv));
+  a.exact_sqrt = c->opts.exact_sqrt != 0;
+  if (const char* kv = std::getenv("DYMU_EXACT_SQRT")) a.exact_sqrt = std::atoi(kv) != 0;
   a.shard_cap = ntiles;
   a.tile_epoch = c->d_tile_epoch;
   a.stats = c->d_stats;

@@ -55,6 +55,8 @@ struct PassArgs {
   unsigned long long* trace;  // debug: kTracePts s_memrealtime stamps per block, or null
   uint32_t sweep_deadline;  // kernel 5 (dyn): > 0: a visit stops sweeping this many 10-ns ticks
                             // after its workgroup started the pass (re-queued as if capped)
+  int exact_sqrt;  // kernel 5 (dyn): 1 = correctly rounded sweep sqrt (10 VALU), 0 = one
+                   // Goldschmidt step (5 VALU, <= 36 ulp)
 };
 
 constexpr int kBins = 64;  // v4/v5 key histogram bins

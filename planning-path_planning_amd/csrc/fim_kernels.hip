@@ -463,6 +463,10 @@ __device__ __forceinline__ double sqrt_cr_fast(double x) {
 
 // sqrt_cr_fast on two independent operands, step-interleaved so the two
 // dependent chains overlap in a single wave (same operations: bit-identical)
+// APPROX: stop after the Goldschmidt step (5 instead of 10 VALU instructions):
+// <= 36 ulp from the correctly rounded sqrt (tools/sqrt_probe.hip: 805 M operands
+// 2C^2 - d^2, |d| < C, C in 2^-380..2^380), the rsq estimate alone is ~2^-23
+template <bool APPROX = false>
 __device__ __forceinline__ void sqrt_cr_fast2(double x0, double x1, double& r0, double& r1) {
   const double y0 = __builtin_amdgcn_rsq(x0), y1 = __builtin_amdgcn_rsq(x1);
   double s0 = x0 * y0, s1 = x1 * y1;
@@ -470,6 +474,11 @@ __device__ __forceinline__ void sqrt_cr_fast2(double x0, double x1, double& r0, 
   const double e0 = __builtin_fma(-h0, s0, 0.5), e1 = __builtin_fma(-h1, s1, 0.5);
   s0 = __builtin_fma(s0, e0, s0);
   s1 = __builtin_fma(s1, e1, s1);
+  if constexpr (APPROX) {
+    r0 = s0;
+    r1 = s1;
+    return;
+  }
   h0 = __builtin_fma(h0, e0, h0);
   h1 = __builtin_fma(h1, e1, h1);
   double d0 = __builtin_fma(-s0, s0, x0), d1 = __builtin_fma(-s1, s1, x1);
@@ -481,6 +490,14 @@ __device__ __forceinline__ void sqrt_cr_fast2(double x0, double x1, double& r0, 
   r1 = __builtin_fma(d1, h1, s1);
 }
 constexpr double kFastMinF = 0x1p-383;
+
+// the approximate sweep sqrt of sqrt_cr_fast2<true> on one operand (self-test)
+__device__ __forceinline__ double sqrt_gs1(double x) {
+  const double y0 = __builtin_amdgcn_rsq(x);
+  const double s = x * y0;
+  const double e = __builtin_fma(-(y0 * 0.5), s, 0.5);
+  return __builtin_fma(s, e, s);
+}
 
 // One cell of the reference update (:504-537) against the image.  Preconditions
 // (guaranteed by the skip test): f finite and min(Tx,Ty) finite, so the
@@ -515,25 +532,26 @@ __device__ __forceinline__ bool rb_update(double* img, int slot, double f, doubl
 
 // The update of rb_update without the skip test, for the arithmetic self-test
 // (dymu_eikonal_batch): candidate T' from (Tx, Ty, C) as at :531-535.
-template <bool FAST>
+// MODE 0: sqrt(), 1: sqrt_cr_fast (bit-identical), 2: the approximate sweep sqrt
+template <int MODE>
 __device__ __forceinline__ double update_value(double tx_, double ty_, double f) {
   const double m = minnn(tx_, ty_);
   if (!(f < dinf()) || !(m < dinf())) return m + f;  // outside the kernel's fast path
   const double dd = tx_ - ty_;
   if (fabs(dd) < f) {
     const double r = 2.0 * (f * f) - dd * dd;
-    const double sq = FAST ? sqrt_cr_fast(r) : sqrt(r);
+    const double sq = MODE == 2 ? sqrt_gs1(r) : MODE == 1 ? sqrt_cr_fast(r) : sqrt(r);
     return ((tx_ + ty_) + sq) * 0.5;
   }
   return m + f;
 }
 
-template <bool FAST>
+template <int MODE>
 __global__ void k_eikonal_batch(const double* tx, const double* ty, const double* c, double* out,
                                 uint64_t n) {
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
        k += (uint64_t)gridDim.x * blockDim.x)
-    out[k] = update_value<FAST>(tx[k], ty[k], c[k]);
+    out[k] = update_value<MODE>(tx[k], ty[k], c[k]);
 }
 
 template <bool FAST>
@@ -866,7 +884,7 @@ __device__ __forceinline__ int visit8(const PassArgs& a, double* img, unsigned l
 // running one after the other behind per-cell branches.  Same operations as
 // rb_update: bit-identical results (a discarded two-sided candidate may be
 // NaN from a negative radicand; it is never selected).
-template <bool FAST, int PITCH>
+template <bool FAST, int PITCH, bool APPROX = false>
 __device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, double f0,
                                            double f1, double& t0, double& t1, bool& ch0,
                                            bool& ch1) {
@@ -902,7 +920,7 @@ __device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, do
     const double r0 = c20 - d0 * d0, r1 = c21 - d1 * d1;
     double q0, q1;
     if constexpr (FAST) {
-      sqrt_cr_fast2(r0, r1, q0, q1);
+      sqrt_cr_fast2<APPROX>(r0, r1, q0, q1);
     } else {
       q0 = sqrt(r0);
       q1 = sqrt(r1);
@@ -923,7 +941,7 @@ __device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, do
   }
 }
 
-template <bool FAST>
+template <bool FAST, bool APPROX = false>
 __device__ __forceinline__ int rb_sweeps4(double* img, const int (&sr)[2], const int (&sb)[2],
                                           const double (&fr)[2], const double (&fb)[2],
                                           double (&tr)[2], double (&tb)[2], int max_inner,
@@ -938,21 +956,21 @@ __device__ __forceinline__ int rb_sweeps4(double* img, const int (&sr)[2], const
     // two sweeps per convergence test: the second sweep's flags decide (a sweep
     // that changes nothing is the local fixed point)
     __builtin_amdgcn_wave_barrier();
-    rb_update2<FAST, IP16>(img, sr[0], sr[1], fr[0], fr[1], tr[0], tr[1], i0, i1);
+    rb_update2<FAST, IP16, APPROX>(img, sr[0], sr[1], fr[0], fr[1], tr[0], tr[1], i0, i1);
     img[sr[0]] = tr[0];
     img[sr[1]] = tr[1];
     __builtin_amdgcn_wave_barrier();
-    rb_update2<FAST, IP16>(img, sb[0], sb[1], fb[0], fb[1], tb[0], tb[1], i2, i3);
+    rb_update2<FAST, IP16, APPROX>(img, sb[0], sb[1], fb[0], fb[1], tb[0], tb[1], i2, i3);
     img[sb[0]] = tb[0];
     img[sb[1]] = tb[1];
     ++sweeps;
 #endif
     __builtin_amdgcn_wave_barrier();
-    rb_update2<FAST, IP16>(img, sr[0], sr[1], fr[0], fr[1], tr[0], tr[1], i0, i1);
+    rb_update2<FAST, IP16, APPROX>(img, sr[0], sr[1], fr[0], fr[1], tr[0], tr[1], i0, i1);
     img[sr[0]] = tr[0];
     img[sr[1]] = tr[1];
     __builtin_amdgcn_wave_barrier();
-    rb_update2<FAST, IP16>(img, sb[0], sb[1], fb[0], fb[1], tb[0], tb[1], i2, i3);
+    rb_update2<FAST, IP16, APPROX>(img, sb[0], sb[1], fb[0], fb[1], tb[0], tb[1], i2, i3);
     img[sb[0]] = tb[0];
     img[sb[1]] = tb[1];
     ++sweeps;
@@ -971,7 +989,7 @@ struct NoGate {
 
 // gate(): wave-uniform, evaluated after the tile's loads are issued (so a key
 // load the gate waits on overlaps them); false = skip the visit, return -1.
-template <class Gate = NoGate>
+template <bool APPROX = false, class Gate = NoGate>
 __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned long long* ek,
                                        bool has, int tx, int ty, int lane, bool& capped,
                                        Gate gate = Gate(), unsigned long long stop_at = ~0ull) {
@@ -1067,7 +1085,7 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
   const bool fast = __all(!(fr[0] < kFastMinF) && !(fr[1] < kFastMinF) &&
                           !(fb[0] < kFastMinF) && !(fb[1] < kFastMinF));
   const int sweeps =
-      fast ? rb_sweeps4<true>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped, stop_at)
+      fast ? rb_sweeps4<true, APPROX>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped, stop_at)
            : rb_sweeps4<false>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped, stop_at);
   // write back decreased cells; dr/db: the decreased value or +inf.  Keys are
   // non-negative doubles, so the u64 order of their bits (ek) is their f64
@@ -1315,7 +1333,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_prio(PassArgs a) {
 // bin) or visits it.  No classify phase and no block-wide barrier between
 // reading the list and the sweeps: a wave that drew a deferred or a quickly
 // converging tile moves on to the next entry while the others still sweep.
-template <int WPB>
+template <int WPB, bool APPROX>
 __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   constexpr int IMG = (16 + 2) * IP16;
   __shared__ uint32_t s_q[QCAP];
@@ -1422,7 +1440,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     if (lane < 4) ek[lane] = kInfBits;
     if (trace && tid == 0 && first) trace[6] = __builtin_amdgcn_s_memrealtime();
     bool capped = false;
-    const int sweeps = visit16(
+    const int sweeps = visit16<APPROX>(
         a, img, ek, true, tx, ty, lane, capped,
         [&] { return key_bin(bitsd(kb), origin_in, inv_delta) <= bstar; }, stop_at);
     if (lane == 0) a.key_in[tile] = kInfBits;
@@ -1733,15 +1751,21 @@ hipError_t launch_prio16_wpb(const PassArgs& a, int blocks, hipStream_t st, hipE
   return hipGetLastError();
 }
 
+template <int WPB, bool APPROX>
+hipError_t launch_dyn_k(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
+                        hipEvent_t e1) {
+  if (e0 || e1)
+    hipExtLaunchKernelGGL((k_fim_pass_dyn<WPB, APPROX>), dim3(blocks), dim3(64 * WPB), 0, st, e0,
+                          e1, 0, a);
+  else
+    hipLaunchKernelGGL((k_fim_pass_dyn<WPB, APPROX>), dim3(blocks), dim3(64 * WPB), 0, st, a);
+  return hipGetLastError();
+}
 template <int WPB>
 hipError_t launch_dyn_wpb(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
                           hipEvent_t e1) {
-  if (e0 || e1)
-    hipExtLaunchKernelGGL((k_fim_pass_dyn<WPB>), dim3(blocks), dim3(64 * WPB), 0, st, e0, e1, 0,
-                          a);
-  else
-    hipLaunchKernelGGL((k_fim_pass_dyn<WPB>), dim3(blocks), dim3(64 * WPB), 0, st, a);
-  return hipGetLastError();
+  return a.exact_sqrt ? launch_dyn_k<WPB, false>(a, blocks, st, e0, e1)
+                      : launch_dyn_k<WPB, true>(a, blocks, st, e0, e1);
 }
 
 hipError_t launch_pass_prio16(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
@@ -1763,13 +1787,13 @@ int prio16_blocks_per_cu(int wpb, int dyn) {
   hipError_t e = hipErrorInvalidValue;
   if (dyn) switch (wpb) {
       case 8:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_dyn<8>, 512, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_dyn<8, true>, 512, 0);
         break;
       case 16:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_dyn<16>, 1024, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_dyn<16, true>, 1024, 0);
         break;
       default:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_dyn<4>, 256, 0);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_dyn<4, true>, 256, 0);
     }
   else switch (wpb) {
     case 8:
@@ -1835,11 +1859,14 @@ hipError_t launch_eikonal_batch(const double* tx, const double* ty, const double
   uint64_t blocks = (n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks == 0) return hipSuccess;
-  if (fast)
-    hipLaunchKernelGGL(k_eikonal_batch<true>, dim3((unsigned)blocks), dim3(256), 0, st, tx, ty, c,
+  if (fast == 2)
+    hipLaunchKernelGGL(k_eikonal_batch<2>, dim3((unsigned)blocks), dim3(256), 0, st, tx, ty, c,
+                       out, n);
+  else if (fast)
+    hipLaunchKernelGGL(k_eikonal_batch<1>, dim3((unsigned)blocks), dim3(256), 0, st, tx, ty, c,
                        out, n);
   else
-    hipLaunchKernelGGL(k_eikonal_batch<false>, dim3((unsigned)blocks), dim3(256), 0, st, tx, ty,
+    hipLaunchKernelGGL(k_eikonal_batch<0>, dim3((unsigned)blocks), dim3(256), 0, st, tx, ty,
                        c, out, n);
   return hipGetLastError();
 }

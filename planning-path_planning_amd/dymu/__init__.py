@@ -51,6 +51,7 @@ class DymuOpts(ctypes.Structure):
         ("grid_blocks", ctypes.c_int),
         ("kernel", ctypes.c_int),
         ("prio_target", ctypes.c_int),
+        ("exact_sqrt", ctypes.c_int),
     ]
 
 
@@ -178,11 +179,11 @@ class Engine:
 
     def __init__(self, device: int = -1, passes_per_check: int = 0, max_passes: int = 0,
                  max_inner: int = 0, grid_blocks: int = 0, kernel: int = 0,
-                 prio_target: int = 0):
+                 prio_target: int = 0, exact_sqrt: int = 0):
         lib = load_fim()
         self._lib = lib
         opts = DymuOpts(device, passes_per_check, max_passes, max_inner, grid_blocks, kernel,
-                        prio_target)
+                        prio_target, exact_sqrt)
         ctx = _vp()
         rc = lib.dymu_create(ctypes.byref(ctx), ctypes.byref(opts))
         if rc != DYMU_OK:
@@ -295,8 +296,10 @@ class Engine:
         return st.as_dict()
 
     def eikonal_batch(self, tx: np.ndarray, ty: np.ndarray, c: np.ndarray,
-                      fast: bool = True) -> np.ndarray:
-        """The kernels' update arithmetic on the GPU (bit-level self-test)."""
+                      fast=True) -> np.ndarray:
+        """The kernels' update arithmetic on the GPU (bit-level self-test).
+        fast: False = sqrt(), True = the correctly rounded sweep sqrt, 2 = the
+        approximate sweep sqrt of kernel 5 (dymu_opts.exact_sqrt = 0)."""
         arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (tx, ty, c)]
         n = arrs[0].size
         ptrs = [self.alloc(8 * n) for _ in range(4)]
@@ -304,7 +307,8 @@ class Engine:
             for p, a in zip(ptrs, arrs):
                 self.h2d(p, a)
             _check(self._lib.dymu_eikonal_batch(self.ctx, ptrs[0], ptrs[1], ptrs[2], ptrs[3], n,
-                                                1 if fast else 0), self.ctx)
+                                                2 if fast == 2 else 1 if fast else 0),
+                   self.ctx)
             out = np.empty(n)
             self.d2h(out, ptrs[3])
             return out

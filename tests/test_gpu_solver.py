@@ -178,6 +178,45 @@ def test_update_arithmetic_bit_exact(engine, oracle, fast):
     assert np.array_equal(out, r)
 
 
+def test_update_arithmetic_approx_sqrt(engine):
+    """Kernel 5's default sweep sqrt (one Goldschmidt step after v_rsq_f64,
+    dymu_opts.exact_sqrt = 0): the candidate is within 36 ulp of the reference
+    formula's sqrt term (tools/sqrt_probe.hip), i.e. <= 1e-14 relative; the
+    one-sided and infinite cases are bit-identical."""
+    rng = np.random.default_rng(11)
+    n = 1 << 21
+    c = np.exp(rng.uniform(np.log(1e-3), np.log(1e3), n))
+    tx = rng.uniform(0, 1e4, n)
+    ty = np.abs(tx + rng.normal(0, 1, n) * c)
+    tx[::97] = np.inf
+    ty[::89] = np.inf
+    out = engine.eikonal_batch(tx, ty, c, fast=2)
+    with np.errstate(invalid="ignore"):
+        d = tx - ty
+        two = (np.abs(d) < c) & np.isfinite(tx) & np.isfinite(ty)
+        q = np.sqrt(2 * (c * c) - d * d)
+        r = np.where(two, (tx + ty + q) / 2, np.minimum(tx, ty) + c)
+    assert np.array_equal(out[~two], r[~two])
+    # |error| <= 36 ulp of the sqrt term, halved by the final * 0.5
+    ulp = np.spacing(q[two])
+    assert np.all(np.abs(out[two] - r[two]) <= 18 * ulp + np.spacing(r[two]))
+    assert np.max(np.abs(out[two] - r[two]) / r[two]) <= 1e-14
+
+
+def test_exact_sqrt_option(dymu, oracle):
+    """dymu_opts.exact_sqrt = 1 (kernel 5 with the correctly rounded sweep sqrt)
+    and the default both meet the parity bar on the same grid."""
+    N = 1024
+    F = oracle.synth_speed(N, N, seed=5, obst_frac=0.02, obst_seed=9, goal=(300, 700))
+    Tref, _ = oracle.fmm(F, (300, 700))
+    for ex in (0, 1):
+        eng = dymu.Engine(kernel=5, exact_sqrt=ex)
+        try:
+            assert_parity(eng.solve(F, 300, 700).T, Tref)
+        finally:
+            eng.close()
+
+
 def test_sampled_pass_timing(dymu, oracle):
     """dymu_set_profiling(period) times every period-th pass launch."""
     nx = ny = 512
