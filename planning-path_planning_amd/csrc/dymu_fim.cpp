@@ -217,10 +217,12 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
                              3ull * kShards * kBins, c->d_prio,
                              reinterpret_cast<double*>(c->d_prio + 3), prio_delta(c), c->prio_kappa,
                              st));
-    // default per pass: 64 8x8 tiles per CU (v4) / 8 16x16 tiles per CU (v5),
-    // the measured optima at 8192^2..16384^2
+    // default per pass: 64 8x8 tiles per CU (v4) / 8 16x16 tiles per CU (v5), the
+    // measured optima at 8192^2..16384^2; 4 per CU for whole grids below 2^17 16x16
+    // tiles (4096^2: 6.28 vs 6.50 ms, v11)
+    const bool small5 = D.variant == 5 && !ghost_lo && !ghost_hi && ntiles < (1u << 17);
     a.target = c->prio_target ? c->prio_target
-                              : (uint32_t)c->cu_count * (D.variant == 5 ? 8u : 64u);
+                              : (uint32_t)c->cu_count * (D.variant == 5 ? (small5 ? 4u : 8u) : 64u);
     a.target_frac = c->prio_frac;
     a.prune = c->prune;
     a.delta = prio_delta(c);
@@ -241,11 +243,12 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   a.nty = (int)nty;
   a.ghost_lo = ghost_lo;
   a.ghost_hi = ghost_hi;
-  // v5: a sweep cap of 16 bounds the visit (capped tiles re-queue themselves); from
-  // 2^20 tiles (16384^2) a pass is ended by the capped visits of the busiest SIMDs,
-  // so there a visit also stops sweeping 14 us into the pass (re-queued like a capped
-  // one): 46.0 vs 49.2 ms at 16384^2; at 4096^2 it costs 2%
-  const bool big = ntiles >= (1u << 20);
+  // v5: a sweep cap of 16 bounds the visit (capped tiles re-queue themselves); on large
+  // grids a pass is ended by the capped visits of the busiest SIMDs, so there a visit
+  // also stops sweeping 14 us into the pass (re-queued like a capped one): 46.0 vs
+  // 49.2 ms at 16384^2 (v9), 15.6 vs 16.0 ms at 8192^2 (v11).  Whole grids from 2^18
+  // tiles; slabs (more exchange rounds with it) only from 2^20.
+  const bool big = ntiles >= (1u << 20) || (!ghost_lo && !ghost_hi && ntiles >= (1u << 18));
   a.max_inner = c->opts.max_inner > 0 ? c->opts.max_inner
                 : variant == 5            ? 16
                                           : 4 * (TWd + THd);
