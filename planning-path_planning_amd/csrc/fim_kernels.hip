@@ -491,12 +491,17 @@ __device__ __forceinline__ void sqrt_cr_fast2(double x0, double x1, double& r0, 
 }
 constexpr double kFastMinF = 0x1p-383;
 
-// the approximate sweep sqrt of sqrt_cr_fast2<true> on one operand (self-test)
-__device__ __forceinline__ double sqrt_gs1(double x) {
-  const double y0 = __builtin_amdgcn_rsq(x);
-  const double s = x * y0;
-  const double e = __builtin_fma(-(y0 * 0.5), s, 0.5);
-  return __builtin_fma(s, e, s);
+// Kernel 5's default two-sided candidate (Tx + Ty + sqrt(2C^2 - d^2)) / 2 with the
+// Goldschmidt step of sqrt_cr_fast2<true> folded into the combine: with y0 = rsq(r),
+// s = r*y0, sqrt(r) ~ s*(1.5 - 0.5*y0*s), so u = (Tx+Ty)/2 + s*(0.75 - (y0/4)*s);
+// r = fma(-d, d, 2C^2) (one rounding; r >= C^2 on this branch, no cancellation).
+// 8 VALU after d instead of 10 (11 with the exact sqrt: 15).
+__device__ __forceinline__ double two_sided_approx(double tx, double ty, double d, double c2x2) {
+  const double r = __builtin_fma(-d, d, c2x2);
+  const double y0 = __builtin_amdgcn_rsq(r);
+  const double s = r * y0;
+  const double t = __builtin_fma(-(y0 * 0.25), s, 0.75);
+  return __builtin_fma(s, t, (tx + ty) * 0.5);
 }
 
 // One cell of the reference update (:504-537) against the image.  Preconditions
@@ -540,7 +545,8 @@ __device__ __forceinline__ double update_value(double tx_, double ty_, double f)
   const double dd = tx_ - ty_;
   if (fabs(dd) < f) {
     const double r = 2.0 * (f * f) - dd * dd;
-    const double sq = MODE == 2 ? sqrt_gs1(r) : MODE == 1 ? sqrt_cr_fast(r) : sqrt(r);
+    if (MODE == 2) return two_sided_approx(tx_, ty_, dd, 2.0 * (f * f));
+    const double sq = MODE == 1 ? sqrt_cr_fast(r) : sqrt(r);
     return ((tx_ + ty_) + sq) * 0.5;
   }
   return m + f;
@@ -917,16 +923,25 @@ __device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, do
   {
 #endif
     const double d0 = tx0 - ty0, d1 = tx1 - ty1;
-    const double r0 = c20 - d0 * d0, r1 = c21 - d1 * d1;
-    double q0, q1;
-    if constexpr (FAST) {
-      sqrt_cr_fast2<APPROX>(r0, r1, q0, q1);
+    double v0, v1;  // two-sided candidates
+    if constexpr (FAST && APPROX) {
+      // an obstacle (f = inf) gives NaN here (rsq(inf) * inf), which v_min ignores
+      v0 = two_sided_approx(tx0, ty0, d0, c20);
+      v1 = two_sided_approx(tx1, ty1, d1, c21);
     } else {
-      q0 = sqrt(r0);
-      q1 = sqrt(r1);
+      const double r0 = c20 - d0 * d0, r1 = c21 - d1 * d1;
+      double q0, q1;
+      if constexpr (FAST) {
+        sqrt_cr_fast2<APPROX>(r0, r1, q0, q1);
+      } else {
+        q0 = sqrt(r0);
+        q1 = sqrt(r1);
+      }
+      v0 = ((tx0 + ty0) + q0) * 0.5;
+      v1 = ((tx1 + ty1) + q1) * 0.5;
     }
-    const double u0 = fabs(d0) < f0 ? ((tx0 + ty0) + q0) * 0.5 : m0 + f0;
-    const double u1 = fabs(d1) < f1 ? ((tx1 + ty1) + q1) * 0.5 : m1 + f1;
+    const double u0 = fabs(d0) < f0 ? v0 : m0 + f0;
+    const double u1 = fabs(d1) < f1 ? v1 : m1 + f1;
     ch0 = need0 && u0 < t0;
     ch1 = need1 && u1 < t1;
 #if DYMU_GATE

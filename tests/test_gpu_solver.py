@@ -179,10 +179,11 @@ def test_update_arithmetic_bit_exact(engine, oracle, fast):
 
 
 def test_update_arithmetic_approx_sqrt(engine):
-    """Kernel 5's default sweep sqrt (one Goldschmidt step after v_rsq_f64,
-    dymu_opts.exact_sqrt = 0): the candidate is within 36 ulp of the reference
-    formula's sqrt term (tools/sqrt_probe.hip), i.e. <= 1e-14 relative; the
-    one-sided and infinite cases are bit-identical."""
+    """Kernel 5's default two-sided candidate (dymu_opts.exact_sqrt = 0: one
+    Goldschmidt step after v_rsq_f64, folded into the combine; two_sided_approx)
+    is within 18 ulp of the sqrt term of the reference formula plus one rounding
+    (tools/sqrt_probe.hip), i.e. <= 1e-14 relative; the one-sided and infinite
+    cases are bit-identical."""
     rng = np.random.default_rng(11)
     n = 1 << 21
     c = np.exp(rng.uniform(np.log(1e-3), np.log(1e3), n))

@@ -1,6 +1,7 @@
 // sqrt_probe.hip -- ulp error of the pass kernel's sqrt variants vs the correctly
 // rounded sqrt on gfx950, over x = 2C^2 - d^2 with |d| < C (the sweep's operands):
-// raw v_rsq_f64 * x, one Goldschmidt step (DYMU_SQRT 2), plus one Newton step (1).
+// raw v_rsq_f64 * x, one Goldschmidt step, plus one Newton step; and the kernel's
+// fused two-sided candidate (two_sided_approx) in ulps of the candidate.
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/sqrt_probe.hip -o tools/sqrt_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -43,7 +44,26 @@ __global__ void k_probe(unsigned long long seed, unsigned long long n, int scale
     const double g1 = s;
     const double dd = __builtin_fma(-s, s, x);
     const double n1 = __builtin_fma(dd, h, s);
-    const double v[3] = {raw, g1, n1};
+    // the candidate u of the kernel's fused form (two_sided_approx) vs the reference
+    // formula ((Tx + Ty) + sqrt(2C^2 - d^2)) / 2 on the kernel's domain: Tx, Ty >= 0,
+    // |Tx - Ty| < C (Tx = T0, Ty = T0 + |d|), so u >= C / sqrt(2)
+    const double T0 = C * 1000.0 * (double)((r1 >> 3) & 0xff) / 255.0;
+    const double tx = T0, ty = T0 + fabs(d), dv = tx - ty;
+    const double c2 = 2.0 * (C * C);
+    const double rr = c2 - dv * dv;
+    const double uref = ((tx + ty) + sqrt(rr)) * 0.5;
+    const double rf = __builtin_fma(-dv, dv, c2);
+    const double yf = __builtin_amdgcn_rsq(rf);
+    const double sf = rf * yf;
+    const double tf = __builtin_fma(-(yf * 0.25), sf, 0.75);
+    const double uf = __builtin_fma(sf, tf, (tx + ty) * 0.5);
+    const double v[4] = {raw, g1, n1, uf};
+    {
+      const long long e2 = ulps(uf, uref);
+      atomicMax(&out[3 * 4 + 0], (unsigned long long)e2);
+      if (e2) atomicAdd(&out[3 * 4 + 1], 1ull);
+    }
+    (void)v;
     for (int k = 0; k < 3; ++k) {
       const long long e2 = ulps(v[k], cr);
       atomicMax(&out[k * 4 + 0], (unsigned long long)e2);
@@ -56,15 +76,16 @@ int main(int argc, char** argv) {
   const unsigned long long n = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : (1ull << 28);
   const int ranges[][2] = {{0, 3}, {-20, 20}, {-380, 380}};
   unsigned long long* d;
-  hipMalloc(&d, sizeof(unsigned long long) * 12);
+  hipMalloc(&d, sizeof(unsigned long long) * 16);
   for (auto& rg : ranges) {
-    hipMemset(d, 0, sizeof(unsigned long long) * 12);
+    hipMemset(d, 0, sizeof(unsigned long long) * 16);
     hipLaunchKernelGGL(k_probe, dim3(4096), dim3(256), 0, 0, 0x1234ull + rg[0], n, rg[0], rg[1], d);
-    unsigned long long h[12];
+    unsigned long long h[16];
     if (hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-    const char* nm[3] = {"raw x*rsq", "1 Goldschmidt (DYMU_SQRT 2)", "+1 Newton (DYMU_SQRT 1)"};
+    const char* nm[4] = {"raw x*rsq", "1 Goldschmidt step", "+1 Newton step",
+                         "fused candidate u (ulp of u)"};
     std::printf("C in [2^%d, 2^%d), %llu samples\n", rg[0], rg[1], n);
-    for (int k = 0; k < 3; ++k)
+    for (int k = 0; k < 4; ++k)
       std::printf("  %-30s max %llu ulp, %.3e of samples not correctly rounded\n", nm[k], h[k * 4],
                   (double)h[k * 4 + 1] / (double)n);
   }
