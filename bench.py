@@ -116,9 +116,10 @@ def cpu_reference_algorithm(n_edge, obst):
 
 PROFILE_PERIOD = 32  # time every 32nd pass launch with HIP events (sampled mean duration;
 # each sampled launch costs ~4.6 us of event overhead: every 8th added 3% to the solve)
+_EXACT = os.environ.get("DYMU_EXACT_SQRT", "0") not in ("", "0")  # dymu_opts.exact_sqrt
 KERNEL_NAMES = {1: "k_fim_pass(", 2: "k_fim_pass_w8", 3: "k_fim_pass_rb", 4: "k_fim_pass_prio<8>",
-                5: "k_fim_pass_dyn<16>" if os.environ.get("DYMU_DYN", "1") != "0"
-                else "k_fim_pass_prio<16"}
+                5: f"k_fim_pass_dyn<16, {'false' if _EXACT else 'true'}>"
+                if os.environ.get("DYMU_DYN", "1") != "0" else "k_fim_pass_prio<16"}
 
 
 def run_single(args):

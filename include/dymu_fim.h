@@ -63,8 +63,9 @@ typedef struct dymu_opts {
                            (64 per CU for 4, 8 per CU for 5) */
   int exact_sqrt;       /* kernel 5: 1 = correctly rounded sqrt in the sweeps (every update
                            bit-identical to the reference formula); 0 = default: one
-                           Goldschmidt step, <= 36 ulp on the sqrt term, solve error vs the
-                           reference FMM unchanged (<= 6e-15 rel) */
+                           Goldschmidt step folded into the candidate, <= 36 ulp of the
+                           reference candidate, solve error vs the reference FMM unchanged
+                           (<= 6e-15 rel) */
 } dymu_opts;
 
 typedef struct dymu_stats {

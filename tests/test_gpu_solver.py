@@ -181,9 +181,9 @@ def test_update_arithmetic_bit_exact(engine, oracle, fast):
 def test_update_arithmetic_approx_sqrt(engine):
     """Kernel 5's default two-sided candidate (dymu_opts.exact_sqrt = 0: one
     Goldschmidt step after v_rsq_f64, folded into the combine; two_sided_approx)
-    is within 18 ulp of the sqrt term of the reference formula plus one rounding
-    (tools/sqrt_probe.hip), i.e. <= 1e-14 relative; the one-sided and infinite
-    cases are bit-identical."""
+    is within 36 ulp of the reference formula's candidate (tools/sqrt_probe.hip:
+    805 M operands with Tx, Ty >= 0, max 36 ulp, 0.66% not correctly rounded),
+    i.e. <= 1e-14 relative; the one-sided and infinite cases are bit-identical."""
     rng = np.random.default_rng(11)
     n = 1 << 21
     c = np.exp(rng.uniform(np.log(1e-3), np.log(1e3), n))
@@ -198,9 +198,7 @@ def test_update_arithmetic_approx_sqrt(engine):
         q = np.sqrt(2 * (c * c) - d * d)
         r = np.where(two, (tx + ty + q) / 2, np.minimum(tx, ty) + c)
     assert np.array_equal(out[~two], r[~two])
-    # |error| <= 36 ulp of the sqrt term, halved by the final * 0.5
-    ulp = np.spacing(q[two])
-    assert np.all(np.abs(out[two] - r[two]) <= 18 * ulp + np.spacing(r[two]))
+    assert np.all(np.abs(out[two] - r[two]) <= 40 * np.spacing(r[two]))
     assert np.max(np.abs(out[two] - r[two]) / r[two]) <= 1e-14
 
 
