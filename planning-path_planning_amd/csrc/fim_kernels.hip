@@ -494,14 +494,15 @@ constexpr double kFastMinF = 0x1p-383;
 // Kernel 5's default two-sided candidate (Tx + Ty + sqrt(2C^2 - d^2)) / 2 with the
 // Goldschmidt step of sqrt_cr_fast2<true> folded into the combine: with y0 = rsq(r),
 // s = r*y0, sqrt(r) ~ s*(1.5 - 0.5*y0*s), so u = (Tx+Ty)/2 + s*(0.75 - (y0/4)*s);
-// r = fma(-d, d, 2C^2) (one rounding; r >= C^2 on this branch, no cancellation).
-// 8 VALU after d instead of 10 (11 with the exact sqrt: 15).
-__device__ __forceinline__ double two_sided_approx(double tx, double ty, double d, double c2x2) {
+// r = fma(-d, d, 2C^2) (one rounding; r >= C^2 on this branch, no cancellation) and
+// (Tx+Ty)/2 = fma(d, 0.5, Ty) from the d = Tx - Ty the caller has.
+// 7 VALU after d instead of 10 (the exact sqrt: 15).
+__device__ __forceinline__ double two_sided_approx(double ty, double d, double c2x2) {
   const double r = __builtin_fma(-d, d, c2x2);
   const double y0 = __builtin_amdgcn_rsq(r);
   const double s = r * y0;
   const double t = __builtin_fma(-(y0 * 0.25), s, 0.75);
-  return __builtin_fma(s, t, (tx + ty) * 0.5);
+  return __builtin_fma(s, t, __builtin_fma(d, 0.5, ty));
 }
 
 // One cell of the reference update (:504-537) against the image.  Preconditions
@@ -545,7 +546,7 @@ __device__ __forceinline__ double update_value(double tx_, double ty_, double f)
   const double dd = tx_ - ty_;
   if (fabs(dd) < f) {
     const double r = 2.0 * (f * f) - dd * dd;
-    if (MODE == 2) return two_sided_approx(tx_, ty_, dd, 2.0 * (f * f));
+    if (MODE == 2) return two_sided_approx(ty_, dd, 2.0 * (f * f));
     const double sq = MODE == 1 ? sqrt_cr_fast(r) : sqrt(r);
     return ((tx_ + ty_) + sq) * 0.5;
   }
@@ -926,8 +927,8 @@ __device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, do
     double v0, v1;  // two-sided candidates
     if constexpr (FAST && APPROX) {
       // an obstacle (f = inf) gives NaN here (rsq(inf) * inf), which v_min ignores
-      v0 = two_sided_approx(tx0, ty0, d0, c20);
-      v1 = two_sided_approx(tx1, ty1, d1, c21);
+      v0 = two_sided_approx(ty0, d0, c20);
+      v1 = two_sided_approx(ty1, d1, c21);
     } else {
       const double r0 = c20 - d0 * d0, r1 = c21 - d1 * d1;
       double q0, q1;

@@ -56,7 +56,7 @@ __global__ void k_probe(unsigned long long seed, unsigned long long n, int scale
     const double yf = __builtin_amdgcn_rsq(rf);
     const double sf = rf * yf;
     const double tf = __builtin_fma(-(yf * 0.25), sf, 0.75);
-    const double uf = __builtin_fma(sf, tf, (tx + ty) * 0.5);
+    const double uf = __builtin_fma(sf, tf, __builtin_fma(dv, 0.5, ty));
     const double v[4] = {raw, g1, n1, uf};
     {
       const long long e2 = ulps(uf, uref);
