@@ -3,8 +3,9 @@
 // :186-210 (calculateSlope), :217-293 (calculateNominalCost), :297-308
 // (smoothCost), with quirks Q1-Q4, plus the per-node speed of :527-528.
 //
-// Two HBM-bound elementwise/stencil kernels over the row-major SoA planner
-// state (pitch ld); one thread per cell, grid-stride, coalesced along rows.
+// Two elementwise/stencil kernels over the row-major SoA planner state (pitch
+// ld); one thread per cell, 2-D grid-stride (rows on blockIdx.y, columns on
+// blockIdx.x), coalesced along rows and free of 64-bit index division.
 //   k_cost_nominal: terrain class (border -> 0), slope (3x3 central /
 //     one-sided differences), nominal cost from the LUT, sticky obstacle flag,
 //     locomotion mode, hazard/trafficability of obstacles.
@@ -41,12 +42,15 @@ __device__ __forceinline__ double slope_at(const double* E, int64_t ld, uint32_t
   return atan(sqrt(dx * dx + dy * dy));
 }
 
+// rows j on blockIdx.y, columns i on blockIdx.x (both grid-strided)
+#define DYMU_FOR_CELLS(a)                                                             \
+  for (uint32_t j = blockIdx.y; j < (a).ny; j += gridDim.y)                           \
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (a).nx;              \
+         i += gridDim.x * blockDim.x)
+
 __global__ void k_cost_nominal(CostArgs a) {
-  const uint64_t n = (uint64_t)a.nx * a.ny;
   const double kPi = 3.14159265358979323846;  // M_PI
-  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t j = (uint32_t)(c / a.nx), i = (uint32_t)(c % a.nx);
+  DYMU_FOR_CELLS(a) {
     const int64_t k = (int64_t)j * a.ld + i;
     // :162-163 border cells are terrain 0 (obstacle)
     const uint32_t t = (i == 0 || j == 0 || i == a.nx - 1 || j == a.ny - 1)
@@ -118,10 +122,7 @@ __device__ __forceinline__ double speed(double res, double cost, double hd, doub
 }
 
 __global__ void k_cost_smooth(CostArgs a) {
-  const uint64_t n = (uint64_t)a.nx * a.ny;
-  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t j = (uint32_t)(c / a.nx), i = (uint32_t)(c % a.nx);
+  DYMU_FOR_CELLS(a) {
     const int64_t k = (int64_t)j * a.ld + i;
     const double* R = a.st.raw_cost;
     double csum = a.st.cost[k], nn = 5;  // Q1: starts from the previous cost
@@ -136,33 +137,36 @@ __global__ void k_cost_smooth(CostArgs a) {
 }
 
 __global__ void k_pack_speed(CostArgs a) {
-  const uint64_t n = (uint64_t)a.nx * a.ny;
-  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    const int64_t k = (int64_t)(c / a.nx) * a.ld + (int64_t)(c % a.nx);
+  DYMU_FOR_CELLS(a) {
+    const int64_t k = (int64_t)j * a.ld + i;
     a.F[k] = speed(a.res, a.st.cost[k], a.st.hazard[k], a.st.traff[k], a.st.is_obstacle[k] != 0);
   }
 }
 
-unsigned grid_for(uint64_t n) {
-  uint64_t b = (n + 255) / 256;
-  if (b > 8192) b = 8192;  // grid-stride beyond 32 workgroups per CU
-  return b ? (unsigned)b : 1u;
+// 256-thread rows of workgroups: enough column blocks to cover a row, rows
+// until ~8192 workgroups (32 per CU), grid-stride beyond
+dim3 grid_for(uint32_t nx, uint32_t ny) {
+  const uint32_t gx = nx ? (nx + 255) / 256 : 1u;
+  uint32_t gy = 8192u / gx;
+  if (gy < 1) gy = 1;
+  if (gy > ny) gy = ny ? ny : 1u;
+  if (gy > 65535u) gy = 65535u;
+  return dim3(gx, gy);
 }
 
 }  // namespace
 
 hipError_t launch_cost_map(const CostArgs& a, hipStream_t st) {
-  const unsigned g = grid_for((uint64_t)a.nx * a.ny);
-  hipLaunchKernelGGL(k_cost_nominal, dim3(g), dim3(256), 0, st, a);
+  const dim3 g = grid_for(a.nx, a.ny);
+  hipLaunchKernelGGL(k_cost_nominal, g, dim3(256), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_cost_smooth, dim3(g), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_cost_smooth, g, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_pack_speed(const CostArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(k_pack_speed, dim3(grid_for((uint64_t)a.nx * a.ny)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_pack_speed, grid_for(a.nx, a.ny), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
