@@ -44,15 +44,11 @@ __device__ __forceinline__ double eikonal(double tx, double ty, double c) {
 // resetGlobalNarrowBand, :473-496).  Ghost rows (sharded mode) are included
 // when rows < 0 / >= ny are passed in.
 // ---------------------------------------------------------------------------
+// rows on blockIdx.y, columns on blockIdx.x (grid-strided; no index division)
 __global__ void k_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, int64_t row_hi) {
-  const uint64_t rows = (uint64_t)(row_hi - row_lo);
-  const uint64_t n = rows * nx;
-  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
-       k += (uint64_t)gridDim.x * blockDim.x) {
-    const int64_t r = row_lo + (int64_t)(k / nx);
-    const uint64_t c = k % nx;
-    T[r * (int64_t)ld + (int64_t)c] = dinf();
-  }
+  for (int64_t r = row_lo + blockIdx.y; r < row_hi; r += gridDim.y)
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < nx; c += gridDim.x * blockDim.x)
+      T[r * (int64_t)ld + (int64_t)c] = dinf();
 }
 
 __global__ void k_seed(double* T, uint64_t ld, int64_t gi, int64_t gj, uint32_t* list,
@@ -1533,19 +1529,34 @@ __global__ void k_prio_init(const double* F, int64_t ld, int64_t nx, int64_t ny,
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nhist;
        k += (uint64_t)gridDim.x * blockDim.x)
     hist[k] = 0u;
-  if (blockIdx.x == 0) {
+  if (blockIdx.x == 0) {  // blockDim.x == 256
     __shared__ double s_sum[256];
     __shared__ uint32_t s_cnt[256];
-    const int64_t ncell = nx * ny;
-    const int64_t ns = ncell < 65536 ? ncell : 65536;
+    __shared__ int64_t s_row[256];
+    // sample: up to 256 rows spread over the grid, from each a contiguous segment of
+    // up to 256 cells at a row-dependent offset (thread t reads cell t of every
+    // segment: coalesced, one page per row, 16 rows in flight).  The former scattered
+    // 1-D sample (a page walk per load) took ~250 us of dependent latency.
+    const int64_t sr = ny < 256 ? ny : 256, sc = nx < 256 ? nx : 256;
+    if ((int64_t)threadIdx.x < sr) {
+      const int64_t j = ((int64_t)threadIdx.x * ny) / sr;
+      const int64_t i0 = (((int64_t)threadIdx.x * 97) % 256) * (nx - sc) / 255;
+      s_row[threadIdx.x] = j * ld + i0;
+    }
+    __syncthreads();
     double sum = 0.0;
     uint32_t cnt = 0;
-    for (int64_t k = threadIdx.x; k < ns; k += blockDim.x) {
-      const int64_t c = (k * ncell) / ns;  // strided sample
-      const double f = F[(c / nx) * ld + (c % nx)];
-      if (f < dinf()) {
-        sum += f;
-        ++cnt;
+    if ((int64_t)threadIdx.x < sc) {
+      for (int64_t a0 = 0; a0 < sr; a0 += 16) {
+        double f[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) f[u] = a0 + u < sr ? F[s_row[a0 + u] + threadIdx.x] : dinf();
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (f[u] < dinf()) {
+            sum += f[u];
+            ++cnt;
+          }
       }
     }
     s_sum[threadIdx.x] = sum;
@@ -1714,11 +1725,14 @@ __global__ void k_synth(double* F, uint64_t ld, uint32_t nx, uint32_t ny, uint64
 // ---------------------------------------------------------------------------
 hipError_t launch_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, int64_t row_hi,
                            hipStream_t st) {
-  const uint64_t n = (uint64_t)(row_hi - row_lo) * nx;
-  uint64_t blocks = (n + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
-  if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fill_inf, dim3((unsigned)blocks), dim3(256), 0, st, T, ld, nx, row_lo,
+  const uint64_t rows = row_hi > row_lo ? (uint64_t)(row_hi - row_lo) : 0;
+  if (rows == 0 || nx == 0) return hipSuccess;
+  const uint32_t gx = (nx + 255) / 256;  // a row per column-block strip, ~8192 workgroups
+  uint64_t gy = 8192u / gx;
+  if (gy < 1) gy = 1;
+  if (gy > rows) gy = rows;
+  if (gy > 65535) gy = 65535;
+  hipLaunchKernelGGL(k_fill_inf, dim3(gx, (unsigned)gy), dim3(256), 0, st, T, ld, nx, row_lo,
                      row_hi);
   return hipGetLastError();
 }
