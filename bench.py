@@ -114,8 +114,9 @@ def cpu_reference_algorithm(n_edge, obst):
     }
 
 
-PROFILE_PERIOD = 32  # time every 32nd pass launch with HIP events (sampled mean duration;
-# each sampled launch costs ~4.6 us of event overhead: every 8th added 3% to the solve)
+PROFILE_PERIOD = 64  # time every 64th pass launch with HIP events (sampled mean duration;
+# ~150 launches over 5 steps; each sampled launch costs ~5-8 us of event overhead: every
+# 8th added 3% to the solve, every 32nd 1.3%)
 _EXACT = os.environ.get("DYMU_EXACT_SQRT", "0") not in ("", "0")  # dymu_opts.exact_sqrt
 KERNEL_NAMES = {1: "k_fim_pass(", 2: "k_fim_pass_w8", 3: "k_fim_pass_rb", 4: "k_fim_pass_prio<8>",
                 5: f"k_fim_pass_dyn<16, {'false' if _EXACT else 'true'}>"

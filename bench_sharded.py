@@ -16,7 +16,7 @@ import torch.distributed as dist
 
 import dymu
 
-PROFILE_PERIOD = 32  # time every 32nd pass launch of rank 0 (bench.py's roofline)
+PROFILE_PERIOD = 64  # time every 64th pass launch of rank 0 (bench.py's roofline)
 
 
 def _env_defaults():
