@@ -44,11 +44,24 @@ __device__ __forceinline__ double eikonal(double tx, double ty, double c) {
 // resetGlobalNarrowBand, :473-496).  Ghost rows (sharded mode) are included
 // when rows < 0 / >= ny are passed in.
 // ---------------------------------------------------------------------------
-// rows on blockIdx.y, columns on blockIdx.x (grid-strided; no index division)
+// rows on blockIdx.y, columns on blockIdx.x (grid-strided; no index division);
+// 16-byte stores (two cells per lane) on rows that start 16-byte aligned
 __global__ void k_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, int64_t row_hi) {
-  for (int64_t r = row_lo + blockIdx.y; r < row_hi; r += gridDim.y)
-    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < nx; c += gridDim.x * blockDim.x)
-      T[r * (int64_t)ld + (int64_t)c] = dinf();
+  const double inf = dinf();
+  for (int64_t r = row_lo + blockIdx.y; r < row_hi; r += gridDim.y) {
+    double* row = T + r * (int64_t)ld;
+    if (((uintptr_t)row & 15) == 0) {  // wave-uniform
+      double2* row2 = reinterpret_cast<double2*>(row);
+      for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < nx / 2;
+           c += gridDim.x * blockDim.x)
+        row2[c] = make_double2(inf, inf);
+      if ((nx & 1) && blockIdx.x == 0 && threadIdx.x == 0) row[nx - 1] = inf;
+    } else {
+      for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < nx;
+           c += gridDim.x * blockDim.x)
+        row[c] = inf;
+    }
+  }
 }
 
 __global__ void k_seed(double* T, uint64_t ld, int64_t gi, int64_t gj, uint32_t* list,
@@ -1727,7 +1740,8 @@ hipError_t launch_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, 
                            hipStream_t st) {
   const uint64_t rows = row_hi > row_lo ? (uint64_t)(row_hi - row_lo) : 0;
   if (rows == 0 || nx == 0) return hipSuccess;
-  const uint32_t gx = (nx + 255) / 256;  // a row per column-block strip, ~8192 workgroups
+  const uint32_t gx = (nx / 2 + 255) / 256 + 1;  // a row per column-block strip (2 cells
+                                                // per lane when aligned), ~8192 workgroups
   uint64_t gy = 8192u / gx;
   if (gy < 1) gy = 1;
   if (gy > rows) gy = rows;
