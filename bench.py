@@ -64,7 +64,27 @@ def parse():
                          "python loop; tools/vdist_rehearsal.py)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the row-slab path even at N=1 (exercises the RCCL code path)")
+    ap.add_argument("--fake-cpu", action="store_true",
+                    help="tests only: the N-rank plumbing on CPU (gloo, numpy stand-in engine, "
+                         "python exchange loop); no GPU is touched")
     return ap.parse_args()
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` run without a launcher: start the N rank processes with
+    torch.distributed.run (one per GPU) as children -- this process never touches the
+    GPU -- and return their exit code.  Rank 0's JSON line is the run's output."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def cpu_baseline(n_edge, obst):
@@ -118,9 +138,8 @@ PROFILE_PERIOD = 64  # time every 64th pass launch with HIP events (sampled mean
 # ~150 launches over 5 steps; each sampled launch costs ~5-8 us of event overhead: every
 # 8th added 3% to the solve, every 32nd 1.3%)
 _EXACT = os.environ.get("DYMU_EXACT_SQRT", "0") not in ("", "0")  # dymu_opts.exact_sqrt
-KERNEL_NAMES = {1: "k_fim_pass(", 2: "k_fim_pass_w8", 3: "k_fim_pass_rb", 4: "k_fim_pass_prio<8>",
-                5: f"k_fim_pass_dyn<16, {'false' if _EXACT else 'true'}>"
-                if os.environ.get("DYMU_DYN", "1") != "0" else "k_fim_pass_prio<16"}
+KERNEL_NAMES = {3: "k_fim_pass_rb", 4: "k_fim_pass_prio<8>",
+                5: f"k_fim_pass_dyn<16, {'false' if _EXACT else 'true'}>"}
 
 
 def run_single(args):
@@ -160,8 +179,18 @@ def run_single(args):
 def main():
     args = parse()
     world = args.gpus
+    env_world = os.environ.get("WORLD_SIZE")
+    if world < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    if env_world is None and world > 1:
+        sys.exit(spawn_ranks(world))
+    if env_world is not None and int(env_world) != world:
+        raise SystemExit(f"bench: WORLD_SIZE={env_world} but --gpus {world}: the line would "
+                         "mislabel the run")
     rank = int(os.environ.get("RANK", "0"))
-    if world > 1 or args.sharded:
+    if args.fake_cpu:
+        args.exchange, args.backend = "python", "gloo"
+    if world > 1 or args.sharded or args.fake_cpu:
         import torch  # noqa: F401  (before dymu: one HIP runtime in the process)
         import bench_sharded
 
@@ -264,11 +293,15 @@ def main():
             "tile_visits_per_solve": tot["tile_visits"] / K,
             "inner_sweeps_per_solve": tot["inner_sweeps"] / K,
             "pass_kernel": st.get("kernel"),
+            "ranks_seen": tot.get("ranks_seen", 1),
+            "slabs": tot.get("slabs", [[0, 0, N]]),
         },
         "roofline": roof,
         "cpu_baseline": None,
     }
-    if world == 1 and args.cpu_sample > 0:
+    if args.fake_cpu:
+        line["data"] = "synthetic; --fake-cpu plumbing rehearsal (numpy engine, not a GPU number)"
+    if world == 1 and args.cpu_sample > 0 and not args.fake_cpu:
         line["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.obst)
         line["cpu_reference_algorithm"] = cpu_reference_algorithm(1024, args.obst)
     print(json.dumps(line), flush=True)

@@ -54,7 +54,13 @@ int dymu_dist_destroy(dymu_dist* d);
  * coordinates); this rank's slab geometry comes from dymu_slab_rows.
  * Collective: every rank calls it with the same nx, ny, goal and
  * passes_per_exchange (0 = 4).  `stream` NULL = the context's stream.
- * Blocks until converged; stats are this rank's (rounds = exchange rounds). */
+ * Blocks until converged; stats are this rank's (rounds = exchange rounds).
+ * Errors: a collective pre-flight first checks every rank's arguments, so a
+ * rank-local argument error returns DYMU_ERR_ARG on every rank.  Any later
+ * error aborts the communicator (ncclCommAbort: peers blocked in an exchange
+ * this rank will not post are released by their own wait timeout,
+ * DYMU_DIST_TIMEOUT_S, default 300 s) and every further solve on this handle
+ * returns DYMU_ERR_STATE. */
 int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t ld, uint32_t nx,
                     uint32_t ny, uint32_t goal_i, uint32_t goal_j, uint32_t passes_per_exchange,
                     void* stream, dymu_stats* stats);
@@ -70,6 +76,10 @@ int dymu_vdist_solve(dymu_ctx* const* ctxs, int world, const double* const* F_sl
                      void* stream, dymu_stats* stats);
 
 const char* dymu_dist_last_error(dymu_dist* d);
+
+/* Ranks in the communicator (ncclCommCount): what RCCL actually sees, for the
+ * bench line's `ranks_seen`. */
+int dymu_dist_comm_count(dymu_dist* d, int* ranks);
 
 #ifdef __cplusplus
 }

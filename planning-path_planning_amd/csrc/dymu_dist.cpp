@@ -27,9 +27,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 // Per-rank exchange buffers: r = the rows received from rank-1 (side 0) and
@@ -37,11 +40,12 @@
 // for two round parities (the host reads round m-1's while round m is queued).
 struct Pipe {
   double* rbuf = nullptr;    // [2 side][cap]
-  int32_t* d_cnt = nullptr;  // [2 parity][2]
+  int32_t* d_cnt = nullptr;  // [2 parity][2], then the pre-flight flag
   uint64_t cap = 0;
   double* r(int side) const { return rbuf + (uint64_t)side * cap; }
   int32_t* tot(int par) const { return d_cnt + 2 * par; }
   int32_t* sum(int par) const { return d_cnt + 2 * par + 1; }
+  int32_t* flag() const { return d_cnt + 4; }
 };
 
 struct dymu_dist {
@@ -49,8 +53,9 @@ struct dymu_dist {
   int device = 0;
   int rank = 0, world = 1;
   ncclComm_t comm = nullptr;
+  bool aborted = false;  // the communicator was aborted after an error (no further solves)
   Pipe pipe;
-  int32_t* h_sum = nullptr;  // pinned [2 parity]
+  int32_t* h_sum = nullptr;  // pinned [2 parity + the pre-flight flag]
   hipEvent_t ev[2] = {nullptr, nullptr};
   std::string last_error;
 };
@@ -139,7 +144,7 @@ int pipe_alloc(Pipe* p, uint64_t nx) {
   if (p->d_cnt) (void)hipFree(p->d_cnt);
   *p = Pipe{};
   if (hipMalloc(&p->rbuf, sizeof(double) * 2 * nx) != hipSuccess ||
-      hipMalloc(&p->d_cnt, sizeof(int32_t) * 4) != hipSuccess)
+      hipMalloc(&p->d_cnt, sizeof(int32_t) * 5) != hipSuccess)
     return DYMU_ERR_NOMEM;
   p->cap = nx;
   return DYMU_OK;
@@ -149,6 +154,28 @@ void pipe_free(Pipe* p) {
   if (p->rbuf) (void)hipFree(p->rbuf);
   if (p->d_cnt) (void)hipFree(p->d_cnt);
   *p = Pipe{};
+}
+
+// Host wait on an event queued behind RCCL work, bounded: a peer that died or
+// left the collective sequence would otherwise block this rank forever.
+// DYMU_DIST_TIMEOUT_S (default 300 s) bounds one wait.
+int wait_event(hipEvent_t ev, std::string* err) {
+  static const double limit_s = [] {
+    const char* kv = std::getenv("DYMU_DIST_TIMEOUT_S");
+    const double v = kv ? std::atof(kv) : 0.0;
+    return v > 0.0 ? v : 300.0;
+  }();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 0;; ++spin) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return DYMU_OK;
+    if (e != hipErrorNotReady) return fail(err, "hipEventQuery", hipGetErrorString(e), DYMU_ERR_HIP);
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    if ((spin & 1023) == 1023 &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s)
+      return fail(err, "dymu_dist_solve", "timed out waiting for the exchange (a peer rank failed?)",
+                  DYMU_ERR_RCCL);
+  }
 }
 
 }  // namespace
@@ -178,7 +205,7 @@ int dymu_dist_create(dymu_dist** out, dymu_ctx* ctx, int device,
     return rc;
   };
   if (hipSetDevice(device) != hipSuccess) return bail(DYMU_ERR_HIP);
-  if (hipHostMalloc(&d->h_sum, sizeof(int32_t) * 2, hipHostMallocDefault) != hipSuccess)
+  if (hipHostMalloc(&d->h_sum, sizeof(int32_t) * 3, hipHostMallocDefault) != hipSuccess)
     return bail(DYMU_ERR_NOMEM);
   for (auto& e : d->ev)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return bail(DYMU_ERR_HIP);
@@ -206,33 +233,37 @@ int dymu_dist_destroy(dymu_dist* d) {
 
 const char* dymu_dist_last_error(dymu_dist* d) { return d ? d->last_error.c_str() : ""; }
 
-int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t ld, uint32_t nx,
-                    uint32_t ny, uint32_t goal_i, uint32_t goal_j, uint32_t K, void* stream,
-                    dymu_stats* stats) {
-  if (!d || nx == 0 || ny == 0 || goal_i >= nx || goal_j >= ny) return DYMU_ERR_ARG;
+int dymu_dist_comm_count(dymu_dist* d, int* ranks) {
+  if (!d || !ranks) return DYMU_ERR_ARG;
+  if (!d->comm) return DYMU_ERR_STATE;
+  int n = 0;
+  if (ncclCommCount(d->comm, &n) != ncclSuccess) return DYMU_ERR_RCCL;
+  *ranks = n;
+  return DYMU_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// The round loop of dymu_dist_solve (the domain is live on entry).  Any error
+// return leaves the communicator in an unknown collective state; the caller
+// aborts it.
+int dist_rounds(dymu_dist* d, const Slab& s, uint32_t nx, uint32_t ny, uint32_t K, void* stream,
+                uint64_t* rounds) {
   std::string* err = &d->last_error;
-  if (K == 0) K = kDefaultK;
-  Slab s;
-  DCALL(make_slab(F_slab, T_buf, ld, nx, ny, goal_j, d->rank, d->world, &s));
-  DHIP(err, hipSetDevice(d->device));
-  if (pipe_alloc(&d->pipe, nx) != DYMU_OK)
-    return fail(err, "pipe_alloc", "out of memory", DYMU_ERR_NOMEM);
   const Pipe& p = d->pipe;
-  // RCCL and the domain primitives share one stream: NULL = the context's
-  if (!stream) stream = dymu_get_stream(d->ctx);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  DCALL(dymu_dom_begin(d->ctx, &s.dom, s.goal_local >= 0 ? goal_i : 0, s.goal_local, stream));
   const uint64_t cap = max_rounds(nx, ny, K) + 2 * kCheckEvery;
   uint64_t m = 0, checks = 0;
   bool done = false;
   for (; !done; ++m) {
-    if (m >= cap) {
-      (void)dymu_dom_finish(d->ctx, stream, nullptr);
-      return fail(err, "dymu_dist_solve", "exchange-round cap reached", DYMU_ERR_NOT_CONVERGED);
-    }
+    if (m >= cap) return fail(err, "dymu_dist_solve", "exchange-round cap reached",
+                              DYMU_ERR_NOT_CONVERGED);
     const bool check = (m % kCheckEvery) == kCheckEvery - 1;
     const int par = (int)(checks & 1);
-    DCALL(dymu_dom_run(d->ctx, K, stream));
+    int rc = dymu_dom_run(d->ctx, K, stream);
+    if (rc) return fail(err, "dymu_dom_run", dymu_last_error(d->ctx), rc);
     if (s.lo || s.hi) {
       DNCCL(err, ncclGroupStart());
       if (s.lo) {
@@ -245,21 +276,85 @@ int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t 
       }
       DNCCL(err, ncclGroupEnd());
     }
-    DCALL(dymu_dom_exchange(d->ctx, s.lo ? p.r(0) : nullptr, s.hi ? p.r(1) : nullptr, p.tot(par),
-                            stream));
+    rc = dymu_dom_exchange(d->ctx, s.lo ? p.r(0) : nullptr, s.hi ? p.r(1) : nullptr, p.tot(par),
+                           stream);
+    if (rc) return fail(err, "dymu_dom_exchange", dymu_last_error(d->ctx), rc);
     if (!check) continue;
     DNCCL(err, ncclAllReduce(p.tot(par), p.sum(par), 1, ncclInt32, ncclSum, d->comm, st));
     DHIP(err, hipMemcpyAsync(d->h_sum + par, p.sum(par), sizeof(int32_t), hipMemcpyDeviceToHost,
                              st));
     DHIP(err, hipEventRecord(d->ev[par], st));
     if (checks >= 1) {  // the previous check's global count; this one stays queued meanwhile
-      DHIP(err, hipEventSynchronize(d->ev[par ^ 1]));
+      rc = wait_event(d->ev[par ^ 1], err);
+      if (rc) return rc;
       done = d->h_sum[par ^ 1] == 0;
     }
     ++checks;
   }
-  DCALL(dymu_dom_finish(d->ctx, stream, stats));
-  if (stats) stats->rounds = m;
+  *rounds = m;
+  return DYMU_OK;
+}
+
+// Collective pre-flight: every rank learns whether every rank can solve, so a
+// rank-local argument error (an empty slab, a null buffer) fails all ranks
+// together instead of leaving the others blocked in their first exchange.
+int preflight(dymu_dist* d, bool ok, hipStream_t st) {
+  std::string* err = &d->last_error;
+  const Pipe& p = d->pipe;
+  d->h_sum[2] = ok ? 1 : 0;
+  DHIP(err, hipMemcpyAsync(p.flag(), d->h_sum + 2, sizeof(int32_t), hipMemcpyHostToDevice, st));
+  DNCCL(err, ncclAllReduce(p.flag(), p.flag(), 1, ncclInt32, ncclMin, d->comm, st));
+  DHIP(err, hipMemcpyAsync(d->h_sum + 2, p.flag(), sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  DHIP(err, hipEventRecord(d->ev[0], st));
+  int rc = wait_event(d->ev[0], err);
+  if (rc) return rc;
+  if (d->h_sum[2] != 1)
+    return fail(err, "dymu_dist_solve", ok ? "another rank rejected its slab" : "invalid slab",
+                DYMU_ERR_ARG);
+  return DYMU_OK;
+}
+
+// After an error inside the collective sequence: abort the communicator (its
+// peers may be blocked in a send/recv this rank will never post), leave the
+// domain, and refuse further solves on this handle.
+int abort_comm(dymu_dist* d, int rc) {
+  if (d->comm) (void)ncclCommAbort(d->comm);
+  d->comm = nullptr;
+  d->aborted = true;
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t ld, uint32_t nx,
+                    uint32_t ny, uint32_t goal_i, uint32_t goal_j, uint32_t K, void* stream,
+                    dymu_stats* stats) {
+  if (!d) return DYMU_ERR_ARG;
+  std::string* err = &d->last_error;
+  if (d->aborted || !d->comm)
+    return fail(err, "dymu_dist_solve", "communicator aborted by an earlier error", DYMU_ERR_STATE);
+  if (K == 0) K = kDefaultK;
+  DHIP(err, hipSetDevice(d->device));
+  if (pipe_alloc(&d->pipe, nx ? nx : 1) != DYMU_OK)
+    return abort_comm(d, fail(err, "pipe_alloc", "out of memory", DYMU_ERR_NOMEM));
+  // RCCL and the domain primitives share one stream: NULL = the context's
+  if (!stream) stream = dymu_get_stream(d->ctx);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  Slab s;
+  const bool ok = nx > 0 && ny > 0 && goal_i < nx && goal_j < ny &&
+                  make_slab(F_slab, T_buf, ld, nx, ny, goal_j, d->rank, d->world, &s) == DYMU_OK;
+  int rc = preflight(d, ok, st);
+  if (rc) return rc == DYMU_ERR_ARG ? rc : abort_comm(d, rc);
+  rc = dymu_dom_begin(d->ctx, &s.dom, s.goal_local >= 0 ? goal_i : 0, s.goal_local, stream);
+  if (rc) return abort_comm(d, fail(err, "dymu_dom_begin", dymu_last_error(d->ctx), rc));
+  uint64_t rounds = 0;
+  rc = dist_rounds(d, s, nx, ny, K, stream, &rounds);
+  const int rf = dymu_dom_finish(d->ctx, stream, stats);
+  if (rc) return abort_comm(d, rc);
+  if (rf) return abort_comm(d, fail(err, "dymu_dom_finish", dymu_last_error(d->ctx), rf));
+  if (stats) stats->rounds = rounds;
   return DYMU_OK;
 }
 

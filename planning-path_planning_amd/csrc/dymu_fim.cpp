@@ -30,9 +30,8 @@ struct dymu_ctx {
   int cu_count = 256;
   uint32_t* d_xchg = nullptr;  // k_exchange's block ticket (zero between launches)
 
-  // 1: 32x32 tile per workgroup, 2: 8x8 tile per wave (Jacobi),
   // 3: two 8x8 tiles per wave (red-black), 4: v3 body + priority passes;
-  // 5: priority passes on 16x16 tiles (one per wave);
+  // 5: priority passes on 16x16 tiles (one per wave, 16-wave workgroups);
   // 0 (default): per domain, 5 from prio_min_tiles 8x8 tiles up, else 3.
   // DYMU_KERNEL overrides
   int variant = 0;
@@ -43,9 +42,7 @@ struct dymu_ctx {
   int prio_trace = -1;       // v4: stamp phases of this pass index (DYMU_PRIO_TRACE)
   unsigned long long* d_trace = nullptr;
   int prune = 1;             // v4/v5 exact activation pruning (DYMU_PRUNE=0 disables)
-  int occupancy[6] = {0, 8, 8, 6, 5, 4};  // pass workgroups per CU (occupancy API)
-  int wpb = 16;  // kernel 5: waves per workgroup (DYMU_WPB: 4, 8, 16)
-  int dyn = 1;   // kernel 5: wave-level dynamic scheduling (DYMU_DYN=0: classify phase)
+  int occupancy[6] = {0, 0, 0, 6, 5, 1};  // pass workgroups per CU (occupancy API)
   // passes before the first convergence read-back (then doubling to 64): 16 saves two
   // host round trips per solve (4096^2: 5.88 vs 5.96 ms; DYMU_FIRST_BATCH)
   uint64_t first_batch = 16;
@@ -120,7 +117,7 @@ int fail_hip(dymu_ctx* c, hipError_t e, const char* what) {
     if (_e != hipSuccess) return fail_hip(ctx, _e, #expr); \
   } while (0)
 
-int ensure_tiles(dymu_ctx* c, uint32_t ntiles) {
+int ensure_tiles(dymu_ctx* c, uint32_t ntiles, hipStream_t st) {
   if (ntiles <= c->tiles_cap) return DYMU_OK;
   if (c->d_lists) (void)hipFree(c->d_lists);
   if (c->d_tile_epoch) (void)hipFree(c->d_tile_epoch);
@@ -129,7 +126,7 @@ int ensure_tiles(dymu_ctx* c, uint32_t ntiles) {
   c->tiles_cap = 0;
   HIPC(c, hipMalloc(&c->d_lists, sizeof(uint32_t) * 3ull * kShards * ntiles));
   HIPC(c, hipMalloc(&c->d_tile_epoch, sizeof(uint32_t) * (uint64_t)ntiles));
-  HIPC(c, hipMemsetAsync(c->d_tile_epoch, 0, sizeof(uint32_t) * (uint64_t)ntiles, c->stream));
+  HIPC(c, hipMemsetAsync(c->d_tile_epoch, 0, sizeof(uint32_t) * (uint64_t)ntiles, st));
   c->tiles_cap = ntiles;
   c->epoch_base = 0;
   return DYMU_OK;
@@ -168,9 +165,24 @@ unsigned long long* prio_keys(dymu_ctx* c, uint64_t q) {
   return c->d_keys + q * (uint64_t)c->dom.ntiles;
 }
 
-int tile_w(int variant) { return variant == 1 ? kTileW : variant == 5 ? 16 : kWaveTile; }
-int tile_h(int variant) { return variant == 1 ? kTileH : variant == 5 ? 16 : kWaveTile; }
+int tile_w(int variant) { return variant == 5 ? 16 : kWaveTile; }
+int tile_h(int variant) { return variant == 5 ? 16 : kWaveTile; }
+bool valid_variant(int v) { return v == 0 || (v >= 3 && v <= 5); }
 bool is_prio(int variant) { return variant == 4 || variant == 5; }
+
+// Passes a domain may run beyond max_passes: converge() checks the cap between
+// batches of up to 64 launches, so epochs up to eb + max_passes + kPassSlack + 2
+// can be stamped; the epoch-wrap guard in dom_begin reserves that many.
+constexpr uint64_t kPassSlack = 64;
+
+// Leave the live domain (error paths included): later domains stamp epochs
+// above every epoch this one used, so no tile_epoch entry can block them.
+void dom_retire(dymu_ctx* c) {
+  auto& D = c->dom;
+  if (!D.live) return;
+  c->epoch_base = D.eb + (uint32_t)D.p + 4u;
+  D.live = false;
+}
 
 // ---- domain primitives (whole grid, or one row slab with ghost rows) ----
 // cold = true: T := +inf (incl. ghost rows) and the goal seeded (a fresh solve);
@@ -192,7 +204,8 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   const uint64_t ntiles64 = (uint64_t)ntx * nty;
   if (ntiles64 >= (1ull << 31)) return DYMU_ERR_ARG;
   const uint32_t ntiles = (uint32_t)ntiles64;
-  int rc = ensure_tiles(c, ntiles);
+  dom_retire(c);  // a domain abandoned mid-solve (an error, or no dom_finish)
+  int rc = ensure_tiles(c, ntiles, st);
   if (rc) return rc;
   if (is_prio(variant) && (rc = ensure_prio(c, ntiles)) != DYMU_OK) return rc;
   auto& D = c->dom;
@@ -200,11 +213,12 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   D.variant = variant;
   D.ntiles = ntiles;
   D.max_passes = c->opts.max_passes > 0 ? (uint64_t)c->opts.max_passes : 4ull * ntiles + 1024ull;
-  if ((uint64_t)c->epoch_base + D.max_passes + 8 >= 0xFFFFFFF0ull) {
+  if ((uint64_t)c->epoch_base + D.max_passes + kPassSlack + 8 >= 0xFFFFFFF0ull) {
     HIPC(c, hipMemsetAsync(c->d_tile_epoch, 0, sizeof(uint32_t) * (uint64_t)ntiles, st));
     c->epoch_base = 0;
   }
   D.eb = c->epoch_base;
+  c->epoch_base = D.eb + 4u;  // the seed's epoch stays used even if a step below fails
   const uint64_t lstride = (uint64_t)kShards * ntiles;
   for (int q = 0; q < 3; ++q) {
     D.lists[q] = c->d_lists + q * lstride;
@@ -274,6 +288,11 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
 int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
   auto& D = c->dom;
   if (!D.live) return DYMU_ERR_STATE;
+  if (D.p + K > D.max_passes + kPassSlack) {  // beyond the epochs dom_begin reserved
+    c->last_error = "pass cap reached before convergence";
+    dom_retire(c);
+    return DYMU_ERR_NOT_CONVERGED;
+  }
   PassArgs& a = D.a;
   const bool prof = c->profiling != 0;
   for (uint64_t k = 0; k < K; ++k, ++D.p) {
@@ -314,11 +333,9 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st) {
       e1 = c->prof_ev[D.prof_used + 1];
       D.prof_used += 2;
     }
-    HIPC(c, D.variant == 1   ? launch_pass(a, D.blocks, st, e0, e1)
-            : D.variant == 2 ? launch_pass_w8(a, D.blocks, st, e0, e1)
-            : D.variant == 4 ? launch_pass_prio(a, D.blocks, st, e0, e1)
-            : D.variant == 5 ? launch_pass_prio16(a, D.blocks, st, e0, e1, c->wpb, c->dyn)
-                              : launch_pass_rb(a, D.blocks, st, e0, e1));
+    HIPC(c, D.variant == 4   ? launch_pass_prio(a, D.blocks, st, e0, e1)
+            : D.variant == 5 ? launch_pass_prio16(a, D.blocks, st, e0, e1)
+                             : launch_pass_rb(a, D.blocks, st, e0, e1));
     ++D.launches;
     if (tr) {
       a.trace = nullptr;
@@ -412,8 +429,8 @@ int dom_exchange(dymu_ctx* c, const double* lo, const double* hi, int32_t* d_tot
 int dom_finish(dymu_ctx* c, hipStream_t st, dymu_stats* stats, double ms) {
   auto& D = c->dom;
   if (!D.live) return DYMU_ERR_STATE;
+  dom_retire(c);
   HIPC(c, hipStreamSynchronize(st));
-  c->epoch_base = D.eb + (uint32_t)D.p + 4u;
   c->last_launches = D.launches;
   c->last_pass_ms = 0.0;
   c->last_timed = 0;
@@ -445,7 +462,6 @@ int dom_finish(dymu_ctx* c, hipStream_t st, dymu_stats* stats, double ms) {
     stats->tile_h = tile_h(D.variant);
     stats->kernel = D.variant;
   }
-  D.live = false;
   return DYMU_OK;
 }
 
@@ -455,16 +471,18 @@ int converge(dymu_ctx* c, hipStream_t st, dymu_stats* stats) {
   uint64_t K = c->opts.passes_per_check > 0 ? (uint64_t)c->opts.passes_per_check : c->first_batch;
   for (;;) {
     int rc = dom_launch(c, K, st);
-    if (rc) return rc;
-    uint64_t pending = 0;
-    rc = dom_pending(c, st, &pending);
-    if (rc) return rc;
-    if (pending == 0) break;
-    if (c->dom.p >= c->dom.max_passes) {
+    if (rc == DYMU_OK) {
+      uint64_t pending = 0;
+      rc = dom_pending(c, st, &pending);
+      if (rc == DYMU_OK && pending == 0) break;
+    }
+    if (rc == DYMU_OK && c->dom.p >= c->dom.max_passes) {
       c->last_error = "pass cap reached before convergence";
-      c->epoch_base = c->dom.eb + (uint32_t)c->dom.p + 4u;
-      c->dom.live = false;
-      return DYMU_ERR_NOT_CONVERGED;
+      rc = DYMU_ERR_NOT_CONVERGED;
+    }
+    if (rc) {
+      dom_retire(c);
+      return rc;
     }
     if (c->opts.passes_per_check <= 0) K = std::min<uint64_t>(K * 2, 64);
   }
@@ -582,25 +600,21 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
       c->cu_count = prop.multiProcessorCount;
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   }
-  if (const char* kv = std::getenv("DYMU_WPB")) c->wpb = std::atoi(kv);
-  if (c->wpb != 4 && c->wpb != 8) c->wpb = 16;
-  if (const char* kv = std::getenv("DYMU_DYN")) c->dyn = std::atoi(kv) != 0;
   if (const char* kv = std::getenv("DYMU_FIRST_BATCH"))
     c->first_batch = (uint64_t)std::max(1, std::atoi(kv));
   if (e == hipSuccess) {
-    for (int v = 1; v <= 5; ++v) c->occupancy[v] = pass_blocks_per_cu(v);
-    c->occupancy[5] = prio16_blocks_per_cu(c->wpb, c->dyn);
+    for (int v = 3; v <= 5; ++v) c->occupancy[v] = pass_blocks_per_cu(v);
   }
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
-  if (c->opts.kernel < 0 || c->opts.kernel > 5 || c->opts.prio_target < 0) {
+  if (!valid_variant(c->opts.kernel) || c->opts.prio_target < 0) {
     dymu_destroy(c);
     return DYMU_ERR_ARG;
   }
   c->variant = c->opts.kernel;
   if (const char* kv = std::getenv("DYMU_KERNEL")) {  // development override
     const int v = std::atoi(kv);
-    c->variant = (v >= 0 && v <= 5) ? v : 0;
+    c->variant = valid_variant(v) ? v : 0;
   }
   if (e == hipSuccess) {
     c->prio_target = (uint32_t)c->opts.prio_target;

@@ -6,9 +6,7 @@
 
 namespace dymu {
 
-constexpr int kTileW = 32;  // v1 tile width  (x, columns)
-constexpr int kTileH = 32;  // v1 tile height (y, rows)
-constexpr int kWaveTile = 8;  // v2: one 64-lane wave owns an 8x8 tile, one cell per lane
+constexpr int kWaveTile = 8;  // kernels 3/4: 8x8 tiles, two per 64-lane wave (half-wave each)
 constexpr int kShards = 16;   // active lists are split in shards to spread the append atomics
 
 enum StatSlot : int {
@@ -26,7 +24,7 @@ struct PassArgs {
   int64_t nx, ny;   // local domain
   int ntx, nty;     // tiles
   int ghost_lo;     // row -1 exists in memory (read-only halo)
-  int ghost_hi;     // row ny exists in memory (requires ny % kTileH == 0)
+  int ghost_hi;     // row ny exists in memory (requires ny % tile height == 0)
   int max_inner;    // cap on in-tile sweeps per visit
   uint32_t epoch;   // epoch stamped on tiles enqueued for the NEXT pass
   uint32_t shard_cap;  // capacity of one shard (= number of tiles)
@@ -61,7 +59,7 @@ struct PassArgs {
 
 constexpr int kBins = 64;  // v4/v5 key histogram bins
 constexpr int kTracePts = 10;
-// resident 256-thread workgroups per CU of a pass kernel variant (occupancy API)
+// resident workgroups per CU of pass kernel variant 3/4/5 (occupancy API)
 int pass_blocks_per_cu(int variant);
 
 hipError_t launch_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, int64_t row_hi,
@@ -69,16 +67,10 @@ hipError_t launch_fill_inf(double* T, uint64_t ld, uint32_t nx, int64_t row_lo, 
 hipError_t launch_seed(double* T, uint64_t ld, int64_t gi, int64_t gj, uint32_t* list,
                        uint32_t* count, uint32_t* tile_epoch, uint32_t epoch, uint32_t tile,
                        int set_goal, hipStream_t st);
-hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st,
-                      hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);        // v1: 32x32 tile / workgroup
-hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st,
-                      hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);     // v2: 8x8 tile / wave
 hipError_t launch_pass_prio(const PassArgs& a, int blocks, hipStream_t st,
                            hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_pass_prio16(const PassArgs& a, int blocks, hipStream_t st,
-                             hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, int wpb = 16,
-                             int dyn = 0);
-int prio16_blocks_per_cu(int wpb, int dyn);  // occupancy of launch_pass_prio16's workgroups
+                             hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);  // kernel 5
 hipError_t launch_pass_rb(const PassArgs& a, int blocks, hipStream_t st,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);     // v3: 2 x 8x8 tiles / wave, red-black
 hipError_t launch_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,

@@ -77,177 +77,9 @@ __global__ void k_seed(double* T, uint64_t ld, int64_t gi, int64_t gj, uint32_t*
 }
 
 // ---------------------------------------------------------------------------
-// The pass kernel.
-// Thread layout: 256 threads = 32 columns x 8 strips; thread (c, s) owns the
-// 4 cells of column c, rows 4s..4s+3 of the tile, in registers.  The tile's
-// T lives in LDS with a 1-cell halo so horizontal and strip-boundary
-// neighbours are LDS reads; a strip's own vertical neighbours are registers.
-// Sweeps alternate upward / downward inside a strip (Gauss-Seidel within the
-// strip, chaotic in-place across threads: every value read is an upper bound
-// of the fixed point, so any interleaving converges to it).
-// ---------------------------------------------------------------------------
-constexpr int TW = kTileW;  // 32
-constexpr int TH = kTileH;  // 32
-constexpr int RPT = TH / 8; // rows per thread = 4
-constexpr int LDS_W = TW + 2;
-
-// One cell of a strip: neighbours from registers (same strip) or LDS.
-__device__ __forceinline__ bool relax_cell(double (*sT)[LDS_W], double (&t)[RPT],
-                                           const double (&f)[RPT], int s, int c, int k) {
-  const int r = s * RPT + k;
-  const double south = (k == 0) ? sT[r][c + 1] : t[k - 1];
-  const double north = (k == RPT - 1) ? sT[r + 2][c + 1] : t[k + 1];
-  const double west = sT[r + 1][c];
-  const double east = sT[r + 1][c + 2];
-  const double u = eikonal(fmin(west, east), fmin(north, south), f[k]);  // :506, :519
-  if (u < t[k]) {                                                        // :537
-    t[k] = u;
-    sT[r + 1][c + 1] = u;
-    return true;
-  }
-  return false;
-}
-
-__global__ __launch_bounds__(256) void k_fim_pass(PassArgs a) {
-  __shared__ double sT[TH + 2][LDS_W];
-  __shared__ unsigned s_edge;
-
-  const int tid = threadIdx.x;
-  const int c = tid & (TW - 1);  // column in tile
-  const int s = tid >> 5;        // strip 0..7
-  const uint32_t n_active = *a.count_in;
-
-  if (blockIdx.x == 0 && tid == 0) {
-    *a.count_clear = 0u;  // list (p+2)%3: read by pass p-1 (finished), appended by pass p+1
-    for (int q = 1; q < kShards; ++q) a.count_clear[q] = 0u;
-    if (n_active > 0) {
-      atomicAdd(&a.stats[kStatPasses], 1ull);
-      atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
-    }
-  }
-
-  for (uint32_t li = blockIdx.x; li < n_active; li += gridDim.x) {
-    const uint32_t tile = a.list_in[li];
-    const int tx = (int)(tile % (uint32_t)a.ntx);
-    const int ty = (int)(tile / (uint32_t)a.ntx);
-    const int64_t i0 = (int64_t)tx * TW;
-    const int64_t j0 = (int64_t)ty * TH;
-    const int64_t gi = i0 + c;
-    const bool col_ok = gi < a.nx;
-
-    if (tid == 0) s_edge = 0u;
-
-    // ---- load own cells: T into registers + LDS, F into registers ----
-    double t[RPT], f[RPT], t0[RPT];
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int r = s * RPT + k;
-      const int64_t gj = j0 + r;
-      double tv = dinf(), fv = dinf();
-      if (col_ok && gj < a.ny) {
-        const int64_t off = gj * (int64_t)a.ld + gi;
-        tv = a.T[off];
-        fv = a.F[off];
-      }
-      t[k] = tv;
-      t0[k] = tv;
-      f[k] = fv;
-      sT[r + 1][c + 1] = tv;
-    }
-    // ---- halo: rows -1 / TH (threads 0..31 / 32..63), cols -1 / TW (64..127) ----
-    if (tid < 64) {
-      const int hc = tid & 31;
-      const bool top = tid >= 32;
-      const int64_t gj = top ? j0 + TH : j0 - 1;
-      const int64_t gii = i0 + hc;
-      double v = dinf();
-      const bool row_ok = top ? (gj < a.ny || (gj == a.ny && a.ghost_hi))
-                              : (gj >= 0 || a.ghost_lo);
-      if (row_ok && gii < a.nx) v = a.T[gj * (int64_t)a.ld + gii];
-      sT[top ? TH + 1 : 0][hc + 1] = v;
-    } else if (tid < 128) {
-      const int hr = tid & 31;
-      const bool right = tid >= 96;
-      const int64_t gii = right ? i0 + TW : i0 - 1;
-      const int64_t gj = j0 + hr;
-      double v = dinf();
-      if (gii >= 0 && gii < a.nx && gj < a.ny) v = a.T[gj * (int64_t)a.ld + gii];
-      sT[hr + 1][right ? TW + 1 : 0] = v;
-    }
-    __syncthreads();
-
-    // ---- relax to local convergence ----
-    int sweeps = 0;
-    bool capped = true;
-    for (; sweeps < a.max_inner;) {
-      bool changed = false;
-      // alternate upward / downward order inside the strip; both loops are
-      // fully unrolled so t[] / f[] stay in registers (no dynamic indexing)
-      if ((sweeps & 1) == 0) {
-#pragma unroll
-        for (int k = 0; k < RPT; ++k) changed |= relax_cell(sT, t, f, s, c, k);
-      } else {
-#pragma unroll
-        for (int k = RPT - 1; k >= 0; --k) changed |= relax_cell(sT, t, f, s, c, k);
-      }
-      ++sweeps;
-      if (!__syncthreads_or(changed)) {
-        capped = false;
-        break;
-      }
-    }
-
-    // ---- write back + edge-change flags ----
-    unsigned edge = 0u;
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int r = s * RPT + k;
-      if (t[k] < t0[k]) {
-        const int64_t gj = j0 + r;
-        a.T[gj * (int64_t)a.ld + gi] = t[k];
-        if (r == 0) edge |= 1u;       // south neighbour tile (nb4[0])
-        if (c == 0) edge |= 2u;       // west  (nb4[1])
-        if (c == TW - 1) edge |= 4u;  // east  (nb4[2])
-        if (r == TH - 1) edge |= 8u;  // north (nb4[3])
-      }
-    }
-    if (edge) atomicOr(&s_edge, edge);
-    __syncthreads();
-    if (tid < 5) {
-      const unsigned e = s_edge;
-      int ntx = tx, nty = ty;
-      bool want = false;
-      if (tid == 0) { want = (e & 1u) && ty > 0; nty = ty - 1; }
-      else if (tid == 1) { want = (e & 2u) && tx > 0; ntx = tx - 1; }
-      else if (tid == 2) { want = (e & 4u) && tx + 1 < a.ntx; ntx = tx + 1; }
-      else if (tid == 3) { want = (e & 8u) && ty + 1 < a.nty; nty = ty + 1; }
-      else { want = capped; }
-      if (want) {
-        const uint32_t nt = (uint32_t)nty * (uint32_t)a.ntx + (uint32_t)ntx;
-        if (atomicMax(&a.tile_epoch[nt], a.epoch) < a.epoch) {
-          const uint32_t pos = atomicAdd(a.count_out, 1u);
-          a.list_out[pos] = nt;
-        }
-      }
-      if (tid == 0) {
-        atomicAdd(&a.stats[kStatVisits], 1ull);
-        atomicAdd(&a.stats[kStatSweeps], (unsigned long long)sweeps);
-      }
-    }
-    __syncthreads();  // s_edge / sT reuse by the next tile
-  }
-}
-
-
-// ---------------------------------------------------------------------------
-// v2 pass kernel: one 64-lane wave owns one 8x8 tile, one cell per lane
-// (lane = 8*r + c).  Each sweep writes the wave's cells into a per-wave 10x10
-// LDS image that also holds the tile's halo ring, and reads the four
-// neighbours back (in-wave LDS ops execute in order, so no barrier).  The wave relaxes Jacobi sweeps until
-// no lane improves (wave ballot: no barriers at all), so a workgroup's four
-// waves are four independent workers.  Enqueues are aggregated per workgroup
-// in LDS and published with one atomic per workgroup per pass into one of
-// kShards list shards (same-address atomics serialise at ~11 ns each).
+// Active-tile lists: kShards shards, one wave-or-half-wave per tile, enqueues
+// aggregated per workgroup in LDS and published with one atomic per workgroup
+// per pass into one shard (same-address atomics serialise at ~11 ns each).
 // ---------------------------------------------------------------------------
 constexpr int WT = kWaveTile;
 constexpr int QCAP = 1024;  // LDS enqueue buffer per workgroup
@@ -272,155 +104,6 @@ __device__ __forceinline__ uint32_t list_at_wave(const uint32_t* list, uint32_t 
   return list[(uint64_t)k * cap + (li - base)];
 }
 
-__global__ __launch_bounds__(256) void k_fim_pass_w8(PassArgs a) {
-  __shared__ uint32_t s_q[QCAP];
-  __shared__ uint32_t s_pref[kShards + 1];
-  __shared__ uint32_t s_nq, s_base;
-  __shared__ unsigned long long s_visits, s_sweeps;
-  // per-wave 10x10 image of the tile with its halo ring (corners unused)
-  __shared__ double s_img[4][(WT + 2) * (WT + 2)];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wv = tid >> 6;
-  const int r = lane >> 3, c = lane & 7;
-  const uint32_t shard = blockIdx.x % kShards;
-
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (int q = 0; q < kShards; ++q) {
-      s_pref[q] = acc;
-      acc += a.count_in[q];
-    }
-    s_pref[kShards] = acc;
-    s_nq = 0;
-    s_visits = 0;
-    s_sweeps = 0;
-  }
-  __syncthreads();
-  const uint32_t n_active = s_pref[kShards];
-  if (blockIdx.x == 0) {
-    if (tid < kShards) a.count_clear[tid] = 0u;
-    if (tid == 0 && n_active > 0) {
-      atomicAdd(&a.stats[kStatPasses], 1ull);
-      atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
-    }
-  }
-
-  unsigned long long my_visits = 0, my_sweeps = 0;
-  double* img = s_img[wv];
-  const int me = (r + 1) * (WT + 2) + (c + 1);  // own slot in the image
-  const uint32_t nwaves = gridDim.x * 4u;
-  for (uint32_t li = blockIdx.x * 4u + (uint32_t)wv; li < n_active; li += nwaves) {
-    const uint32_t tile = list_at(a.list_in, a.shard_cap, s_pref, li);
-    const int tx = (int)(tile % (uint32_t)a.ntx);
-    const int ty = (int)(tile / (uint32_t)a.ntx);
-    const int64_t i0 = (int64_t)tx * WT, j0 = (int64_t)ty * WT;
-    const int64_t gi = i0 + c, gj = j0 + r;
-    const bool inside = gi < a.nx && gj < a.ny;
-    double t = dinf(), f = dinf();
-    if (inside) {
-      const int64_t off = gj * a.ld + gi;
-      t = a.T[off];
-      f = a.F[off];
-    }
-    // halo ring: lane (r,c) with c==0 / c==7 loads the west / east cell of its
-    // row, lane with r==0 / r==7 the south / north cell of its column.
-    double hx = dinf(), hy = dinf();
-    if (gj < a.ny) {
-      if (c == 0 && i0 > 0) hx = a.T[gj * a.ld + (i0 - 1)];
-      if (c == WT - 1 && i0 + WT < a.nx) hx = a.T[gj * a.ld + (i0 + WT)];
-    }
-    if (gi < a.nx) {
-      if (r == 0 && (j0 > 0 || a.ghost_lo)) hy = a.T[(j0 - 1) * a.ld + gi];
-      if (r == WT - 1) {
-        const int64_t jn = j0 + WT;
-        if (jn < a.ny || (jn == a.ny && a.ghost_hi)) hy = a.T[jn * a.ld + gi];
-      }
-    }
-    if (c == 0) img[me - 1] = hx;
-    if (c == WT - 1) img[me + 1] = hx;
-    if (r == 0) img[me - (WT + 2)] = hy;
-    if (r == WT - 1) img[me + (WT + 2)] = hy;
-    const double t0 = t;
-    int sweeps = 0;
-    bool capped = true;
-    while (sweeps < a.max_inner) {
-      img[me] = t;
-      __builtin_amdgcn_wave_barrier();
-      const double south = img[me - (WT + 2)];
-      const double west = img[me - 1];
-      const double east = img[me + 1];
-      const double north = img[me + (WT + 2)];
-      const double tx_ = minnn(west, east), ty_ = minnn(north, south);
-      bool imp = false;
-      // cheap bound: U >= min(Tx,Ty) + C/sqrt(2) (exact arithmetic); 0.7071 < 1/sqrt(2)
-      // leaves a relative margin ~1e-5*C, far above rounding, so a skipped cell can
-      // never have improved.
-      if (minnn(tx_, ty_) + 0.7071 * f < t) {
-        const double u = eikonal(tx_, ty_, f);  // :531-535
-        if (u < t) {                            // :537
-          t = u;
-          imp = true;
-        }
-      }
-      ++sweeps;
-      __builtin_amdgcn_wave_barrier();
-      if (!__any(imp)) {
-        capped = false;
-        break;
-      }
-    }
-    my_visits += 1;
-    my_sweeps += (unsigned long long)sweeps;
-
-    const bool dec = t < t0;
-    if (dec) a.T[gj * a.ld + gi] = t;
-    const unsigned long long m = __ballot(dec);
-    // lanes 0..4 test one neighbour each: S, W, E, N, self
-    bool want = false;
-    int nx_t = tx, ny_t = ty;
-    if (lane == 0) { want = (m & 0xFFull) && ty > 0; ny_t = ty - 1; }
-    else if (lane == 1) { want = (m & 0x0101010101010101ull) && tx > 0; nx_t = tx - 1; }
-    else if (lane == 2) { want = (m & 0x8080808080808080ull) && tx + 1 < a.ntx; nx_t = tx + 1; }
-    else if (lane == 3) { want = (m & 0xFF00000000000000ull) && ty + 1 < a.nty; ny_t = ty + 1; }
-    else if (lane == 4) { want = capped; }
-    if (want) {
-      const uint32_t nt = (uint32_t)ny_t * (uint32_t)a.ntx + (uint32_t)nx_t;
-      // a plain read filters most duplicates before the atomic decides
-      if (a.tile_epoch[nt] < a.epoch && atomicMax(&a.tile_epoch[nt], a.epoch) < a.epoch) {
-        const uint32_t pos = atomicAdd(&s_nq, 1u);
-        if (pos < QCAP) {
-          s_q[pos] = nt;
-        } else {  // overflow: publish directly
-          const uint32_t gp = atomicAdd(&a.count_out[shard], 1u);
-          a.list_out[(uint64_t)shard * a.shard_cap + gp] = nt;
-        }
-      }
-    }
-  }
-  // per-workgroup publication
-  if (lane == 0 && my_visits) {
-    atomicAdd(&s_visits, my_visits);
-    atomicAdd(&s_sweeps, my_sweeps);
-  }
-  __syncthreads();
-  const uint32_t nq = s_nq < QCAP ? s_nq : QCAP;
-  if (tid == 0) {
-    if (nq) s_base = atomicAdd(&a.count_out[shard], nq);
-    if (s_visits) {
-      unsigned long long* st = a.stats + (uint64_t)shard * kStatSlots;
-      atomicAdd(&st[kStatVisits], s_visits);
-      atomicAdd(&st[kStatSweeps], s_sweeps);
-    }
-  }
-  __syncthreads();
-  for (uint32_t q = tid; q < nq; q += blockDim.x)
-    a.list_out[(uint64_t)shard * a.shard_cap + s_base + q] = s_q[q];
-}
-
-
-
 // ---------------------------------------------------------------------------
 // v3 pass kernel: red-black Gauss-Seidel, two 8x8 tiles per wave.
 // Half-wave h (lanes 32h..32h+31) owns one tile; lane (r = l>>2, q = l&3) owns
@@ -437,12 +120,6 @@ __global__ __launch_bounds__(256) void k_fim_pass_w8(PassArgs a) {
 // and 16 distinct ds_write_b64 banks per 16-lane group (pitch 10 was 2-way).
 constexpr int IP = 12;
 constexpr int IP16 = 20;  // 16x16 image pitch (18 + 2)
-#ifndef DYMU_CHECK2
-#define DYMU_CHECK2 1
-#endif
-#ifndef DYMU_GATE
-#define DYMU_GATE 0
-#endif
 
 // v_min_f64 on operands that are never NaN (T >= 0 or +inf): one instruction,
 // no canonicalisation (the compiler cannot prove no-NaN for fmin).
@@ -910,18 +587,6 @@ __device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, do
   // one wait for all eight (the v_min asm below would otherwise pin reads behind it)
   asm volatile("" : "+v"(w0), "+v"(e0), "+v"(n0), "+v"(so0), "+v"(w1), "+v"(e1), "+v"(n1),
                "+v"(so1));
-#if DYMU_GATE
-  // per-cell constants: the compiler hoists them out of the sweep loop (held
-  // live there, measured faster than recomputing them under the LDS wait)
-  const double k10 = 0.7071 * f0, k11 = 0.7071 * f1;
-  const double c20 = 2.0 * (f0 * f0), c21 = 2.0 * (f1 * f1);
-  const double tx0 = vmin64(w0, e0), ty0 = vmin64(n0, so0);
-  const double tx1 = vmin64(w1, e1), ty1 = vmin64(n1, so1);
-  const double m0 = vmin64(tx0, ty0), m1 = vmin64(tx1, ty1);
-  const bool need0 = m0 + k10 < t0, need1 = m1 + k11 < t1;
-  ch0 = ch1 = false;
-  if (__any(need0 || need1)) {  // wave-uniform
-#else
   // No skip test: u < t alone decides (u >= min + C/sqrt(2) > min + 0.7071 C, so
   // the skip test of rb_update never rejects an improving candidate), and the
   // half-sweep is one straight-line dependent chain without a scalar branch.
@@ -929,9 +594,7 @@ __device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, do
   const double tx0 = vmin64(w0, e0), ty0 = vmin64(n0, so0);
   const double tx1 = vmin64(w1, e1), ty1 = vmin64(n1, so1);
   const double m0 = vmin64(tx0, ty0), m1 = vmin64(tx1, ty1);
-  constexpr bool need0 = true, need1 = true;
   {
-#endif
     const double d0 = tx0 - ty0, d1 = tx1 - ty1;
     double v0, v1;  // two-sided candidates
     if constexpr (FAST && APPROX) {
@@ -952,17 +615,12 @@ __device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, do
     }
     const double u0 = fabs(d0) < f0 ? v0 : m0 + f0;
     const double u1 = fabs(d1) < f1 ? v1 : m1 + f1;
-    ch0 = need0 && u0 < t0;
-    ch1 = need1 && u1 < t1;
-#if DYMU_GATE
-    t0 = ch0 ? u0 : t0;
-    t1 = ch1 ? u1 : t1;
-#else
+    ch0 = u0 < t0;
+    ch1 = u1 < t1;
     // min(t, u) == (u < t ? u : t): one v_min_f64 on the chain to the LDS write
     // (a NaN candidate -- obstacle cells on the FAST path -- leaves t, as v_min does)
     t0 = vmin64(t0, u0);
     t1 = vmin64(t1, u1);
-#endif
   }
 }
 
@@ -977,7 +635,6 @@ __device__ __forceinline__ int rb_sweeps4(double* img, const int (&sr)[2], const
   // its first sweep pair, so every visit makes progress and the solve terminates
   while (sweeps < max_inner && (sweeps == 0 || __builtin_amdgcn_s_memrealtime() < stop_at)) {
     bool i0, i1, i2, i3;
-#if DYMU_CHECK2
     // two sweeps per convergence test: the second sweep's flags decide (a sweep
     // that changes nothing is the local fixed point)
     __builtin_amdgcn_wave_barrier();
@@ -989,7 +646,6 @@ __device__ __forceinline__ int rb_sweeps4(double* img, const int (&sr)[2], const
     img[sb[0]] = tb[0];
     img[sb[1]] = tb[1];
     ++sweeps;
-#endif
     __builtin_amdgcn_wave_barrier();
     rb_update2<FAST, IP16, APPROX>(img, sr[0], sr[1], fr[0], fr[1], tr[0], tr[1], i0, i1);
     img[sr[0]] = tr[0];
@@ -1146,7 +802,7 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
 // chunks, so fewer of them overflow their wave slots into a second round.
 template <int TS, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_prio(PassArgs a) {
-  static_assert(TS == 8 || TS == 16, "tile size");
+  static_assert(TS == 8, "kernel 4: 8x8 tiles (16x16 tiles are kernel 5, k_fim_pass_dyn)");
   constexpr int TPW = TS == 8 ? 2 : 1;  // tiles per wave
   constexpr int SLOTS = WPB * TPW;       // tile slots per workgroup
   constexpr int IMG = TS == 8 ? (WT + 2) * IP : (16 + 2) * IP16;
@@ -1284,10 +940,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_prio(PassArgs a) {
       if (trace && tid == 0 && wb == 0) trace[6] = __builtin_amdgcn_s_memrealtime();
       bool capped;
       int sweeps;
-      if constexpr (TS == 8)
-        sweeps = visit8(a, img, ek, has, tx, ty, r, q, cr, cb, capped);
-      else
-        sweeps = visit16(a, img, ek, has, tx, ty, lane, capped);
+      sweeps = visit8(a, img, ek, has, tx, ty, r, q, cr, cb, capped);
       if (trace && tid == 0 && wb == 0) {
         __builtin_amdgcn_s_waitcnt(0);
         trace[7] = __builtin_amdgcn_s_memrealtime();
@@ -1759,39 +1412,12 @@ hipError_t launch_seed(double* T, uint64_t ld, int64_t gi, int64_t gj, uint32_t*
   return hipGetLastError();
 }
 
-hipError_t launch_pass(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-  if (e0 || e1)  // timestamps taken by the dispatch itself (no extra stream packets)
-    hipExtLaunchKernelGGL(k_fim_pass, dim3(blocks), dim3(256), 0, st, e0, e1, 0, a);
-  else
-    hipLaunchKernelGGL(k_fim_pass, dim3(blocks), dim3(256), 0, st, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_pass_w8(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-  if (e0 || e1)  // timestamps taken by the dispatch itself (no extra stream packets)
-    hipExtLaunchKernelGGL(k_fim_pass_w8, dim3(blocks), dim3(256), 0, st, e0, e1, 0, a);
-  else
-    hipLaunchKernelGGL(k_fim_pass_w8, dim3(blocks), dim3(256), 0, st, a);
-  return hipGetLastError();
-}
-
 hipError_t launch_pass_prio(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
                             hipEvent_t e1) {
   if (e0 || e1)
     hipExtLaunchKernelGGL(k_fim_pass_prio<8>, dim3(blocks), dim3(256), 0, st, e0, e1, 0, a);
   else
     hipLaunchKernelGGL(k_fim_pass_prio<8>, dim3(blocks), dim3(256), 0, st, a);
-  return hipGetLastError();
-}
-
-template <int WPB>
-hipError_t launch_prio16_wpb(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
-                             hipEvent_t e1) {
-  if (e0 || e1)
-    hipExtLaunchKernelGGL((k_fim_pass_prio<16, WPB>), dim3(blocks), dim3(64 * WPB), 0, st, e0, e1,
-                          0, a);
-  else
-    hipLaunchKernelGGL((k_fim_pass_prio<16, WPB>), dim3(blocks), dim3(64 * WPB), 0, st, a);
   return hipGetLastError();
 }
 
@@ -1805,66 +1431,23 @@ hipError_t launch_dyn_k(const PassArgs& a, int blocks, hipStream_t st, hipEvent_
     hipLaunchKernelGGL((k_fim_pass_dyn<WPB, APPROX>), dim3(blocks), dim3(64 * WPB), 0, st, a);
   return hipGetLastError();
 }
-template <int WPB>
-hipError_t launch_dyn_wpb(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
-                          hipEvent_t e1) {
-  return a.exact_sqrt ? launch_dyn_k<WPB, false>(a, blocks, st, e0, e1)
-                      : launch_dyn_k<WPB, true>(a, blocks, st, e0, e1);
-}
-
+// kernel 5: 16-wave workgroups, the sweep sqrt of a.exact_sqrt
 hipError_t launch_pass_prio16(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
-                              hipEvent_t e1, int wpb, int dyn) {
-  if (dyn) switch (wpb) {
-      case 8: return launch_dyn_wpb<8>(a, blocks, st, e0, e1);
-      case 16: return launch_dyn_wpb<16>(a, blocks, st, e0, e1);
-      default: return launch_dyn_wpb<4>(a, blocks, st, e0, e1);
-    }
-  switch (wpb) {
-    case 8: return launch_prio16_wpb<8>(a, blocks, st, e0, e1);
-    case 16: return launch_prio16_wpb<16>(a, blocks, st, e0, e1);
-    default: return launch_prio16_wpb<4>(a, blocks, st, e0, e1);
-  }
-}
-
-int prio16_blocks_per_cu(int wpb, int dyn) {
-  int n = 0;
-  hipError_t e = hipErrorInvalidValue;
-  if (dyn) switch (wpb) {
-      case 8:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_dyn<8, true>, 512, 0);
-        break;
-      case 16:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_dyn<16, true>, 1024, 0);
-        break;
-      default:
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_dyn<4, true>, 256, 0);
-    }
-  else switch (wpb) {
-    case 8:
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_prio<16, 8>, 512, 0);
-      break;
-    case 16:
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_prio<16, 16>, 1024, 0);
-      break;
-    default:
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_prio<16, 4>, 256, 0);
-  }
-  (void)hipGetLastError();
-  return (e == hipSuccess && n > 0) ? n : 1;
+                              hipEvent_t e1) {
+  return a.exact_sqrt ? launch_dyn_k<16, false>(a, blocks, st, e0, e1)
+                      : launch_dyn_k<16, true>(a, blocks, st, e0, e1);
 }
 
 int pass_blocks_per_cu(int variant) {
   int n = 0;
   hipError_t e = hipErrorInvalidValue;
   switch (variant) {
-    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass, 256, 0); break;
-    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_w8, 256, 0); break;
     case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_rb, 256, 0); break;
     case 4:
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_prio<8>, 256, 0);
       break;
     case 5:
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_prio<16>, 256, 0);
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_fim_pass_dyn<16, true>, 1024, 0);
       break;
     default: break;
   }

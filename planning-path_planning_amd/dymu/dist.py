@@ -33,6 +33,7 @@ DIST_SYMBOLS = {
                                 ctypes.POINTER(_vp), _u64, _u32, _u32, _u32, _u32, _u32, _vp,
                                 ctypes.POINTER(DymuStats)]),
     "dymu_dist_last_error": (ctypes.c_char_p, [_vp]),
+    "dymu_dist_comm_count": (_i32, [_vp, ctypes.POINTER(ctypes.c_int)]),
 }
 
 _dl = None
@@ -74,6 +75,14 @@ class DistSolver:
                                         world)
         if rc != 0:
             raise DymuError(rc, "dymu_dist_create (RCCL communicator)")
+
+    def comm_count(self) -> int:
+        """Ranks in the RCCL communicator (ncclCommCount)."""
+        n = ctypes.c_int(0)
+        rc = self._lib.dymu_dist_comm_count(self.h, ctypes.byref(n))
+        if rc != 0:
+            raise DymuError(rc, "dymu_dist_comm_count")
+        return n.value
 
     def close(self):
         if self.h:

@@ -125,6 +125,7 @@ class SlabSolver:
         # the first P2P of an NCCL group must not be a partial one
         self._all_reduce_pending()
         self.exchanges = 0
+        converged = False
         while self.exchanges < max_exchanges:
             self.eng.dom_run(self.K, st)
             self._exchange(T_buf)
@@ -134,7 +135,11 @@ class SlabSolver:
             self.exchanges += 1
             if self.exchanges % self.check_every == 0:
                 if self._all_reduce_pending() == 0:
+                    converged = True
                     break
         stats = self.eng.dom_finish(st)
         stats["rounds"] = self.exchanges
+        if not converged:  # every rank stops at the same exchange count: all raise
+            raise RuntimeError(f"SlabSolver: no global fixed point after {self.exchanges} "
+                               f"exchanges (max_exchanges={max_exchanges})")
         return stats

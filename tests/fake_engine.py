@@ -26,6 +26,36 @@ def eikonal_np(tx, ty, c):
     return np.where(two, u2, u1)
 
 
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64(x):
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & _M64
+    x = ((x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & _M64
+    return x ^ (x >> np.uint64(31))
+
+
+def synth_rows(n, row0, nrows, seed=1, obst_frac=0.0, obst_seed=3, goal=(0, 0)):
+    """Rows [row0, row0+nrows) of the synthetic config-3 speed: numpy
+    restatement of k_synth (fim_kernels.hip) / oracle synth_speed -- U(1,5) from
+    splitmix64(seed ^ k), obstacles where splitmix64(obst_seed ^ k) < obst_frac, the
+    goal's 3x3 kept free."""
+    with np.errstate(over="ignore"):
+        j = np.arange(row0, row0 + nrows, dtype=np.uint64)[:, None]
+        i = np.arange(n, dtype=np.uint64)[None, :]
+        k = j * np.uint64(n) + i
+        u = (_splitmix64(np.uint64(seed) ^ k) >> np.uint64(11)).astype(np.float64) * 2.0**-53
+        F = 1.0 + 4.0 * u
+        if obst_frac > 0:
+            u2 = (_splitmix64(np.uint64(obst_seed) ^ k) >> np.uint64(11)).astype(np.float64)
+            ob = u2 * 2.0**-53 < obst_frac
+            near = (np.abs(i.astype(np.int64) - goal[0]) <= 1) & \
+                (np.abs(j.astype(np.int64) - goal[1]) <= 1)
+            F[ob & ~near] = np.inf
+    return F
+
+
 class FakeEngine:
     def dom_begin(self, F, T, nx, nrows, ld, ghost_lo, ghost_hi, goal_i, goal_j_local,
                   stream=0):
