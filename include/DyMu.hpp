@@ -18,8 +18,11 @@
 //   * the local (sub-grid) layer, CoRa and risk methods are not part of this
 //     library (out of scope); getPath's evaluatePath(0) is then the
 //     identity, as in the reference when no local map exists.
-//   * computeTotalCostMap solves the whole map (the reference stops at the
-//     start node); every reachable cell holds its converged value.
+//   * computeTotalCostMap stops like the reference once the start and its nb4
+//     are final: CLOSED cells hold their converged values, the
+//     narrow band the reference's tentative values (replayed on the host from
+//     the CLOSED values), every other cell +inf; ties between equal total
+//     costs may order differently from the reference's insertion order.
 //   * the node-pointer members (global_narrowband, global_propagated_nodes,
 //     global_goal as globalNode*) do not exist: nodes are SoA arrays.
 //   * a start or goal on the border returns false instead of dereferencing
@@ -81,8 +84,9 @@ class DyMuPathPlanner {
   double getTotalCost(base::Waypoint wInt);
 
   // -- extensions (not in the reference) --
-  // Flat row-major views for FFI callers (ny*nx, index j*nx + i).
-  const double* totalCostData() const { return total_cost_.data(); }
+  // Flat row-major views for FFI callers (ny*nx, index j*nx + i).  The total
+  // cost lives on the device; this downloads whatever the host copy lacks.
+  const double* totalCostData() const;
   unsigned sizeX() const { return nx_; }
   unsigned sizeY() const { return ny_; }
   bool hasGoal() const { return has_goal_; }
@@ -94,16 +98,40 @@ class DyMuPathPlanner {
   int lastSolveKind() const { return incremental_; }
   // Local-layer feedback on the global layer (the writes of
   // src/DyMu_LocalPathRepairing.cpp:264-274 and :389-394), row-major ny*nx.
+  // Only the rows that differ from the current values are re-packed and
+  // uploaded before the next solve.
   bool setHazardDensity(const std::vector<double>& hd);
   bool setTrafficability(const std::vector<double>& tr);
+  // Windowed forms: w x h values (row-major) for cells [i0, i0+w) x [j0, j0+h).
+  bool setHazardDensityWindow(unsigned i0, unsigned j0, unsigned w, unsigned h,
+                              const double* hd);
+  bool setTrafficabilityWindow(unsigned i0, unsigned j0, unsigned w, unsigned h,
+                               const double* tr);
+  // Narrow-band cells left by the last computeTotalCostMap (0 after a full solve).
+  uint64_t lastBandSize() const { return band_size_; }
   // Engine options (device ordinal etc.); takes effect on the next solve.
   void setEngineOptions(const dymu_opts& o);
 
  private:
   uint64_t idx(unsigned i, unsigned j) const { return (uint64_t)j * nx_ + i; }
-  bool solveFull();  // pack F, run the engine, unpack T / state
+  // total cost of cell k: the device map, fetched into the host mirror in blocks
+  // of kBlk x kBlk cells on first read
+  double T(uint64_t k) const;
+  void fetchAll() const;
+  // the reference's node state: CLOSED iff popped by its FMM (finite T not above
+  // the last early-exit limit; every finite cell after a full solve)
+  bool closedCell(uint64_t k) const;
+  void markDirty(unsigned j0, unsigned j1);
+  void ensureEngine();
+  // pack F for the dirty rows, upload the rows whose speed changed; returns false
+  // when nothing changed, else the bounding box of the changed cells
+  bool syncSpeed(unsigned& i0, unsigned& i1, unsigned& j0, unsigned& j1);
+  bool propagate(bool early, unsigned si, unsigned sj);
+  void replayBand(double t_closed, const std::vector<uint64_t>& band, std::vector<double>& out);
   void gradientNode(unsigned i, unsigned j, double& dnx, double& dny) const;
   bool isSafeNode(unsigned i, unsigned j) const;
+
+  static constexpr unsigned kBlk = 128;
 
   // parameters (src/DyMu.hpp:399-427)
   double risk_distance_, reconnect_distance_, risk_ratio_;
@@ -115,22 +143,37 @@ class DyMuPathPlanner {
   std::vector<std::string> locomotion_modes_;
 
   // SoA node fields (globalNode, src/DyMu.hpp:69-108)
-  std::vector<double> elevation_, slope_, raw_cost_, cost_, hazard_, traff_, total_cost_;
+  std::vector<double> elevation_, slope_, raw_cost_, cost_, hazard_, traff_;
   std::vector<uint32_t> terrain_;
-  std::vector<uint8_t> is_obstacle_, state_;
+  std::vector<uint8_t> is_obstacle_;
   std::vector<int32_t> loc_mode_;  // -1 = "DONT_CARE"
-  std::vector<double> heading_unused_;
 
   bool has_goal_ = false;
   unsigned goal_i_ = 0, goal_j_ = 0;
   double goal_heading_ = 0.0;
 
+  // engine and its device-resident map (pitch nx_)
   dymu_ctx* ctx_ = nullptr;
   dymu_opts opts_{-1, 0, 0, 0, 0, 0, 0, 0};
   dymu_stats stats_{};
-  std::vector<double> speed_;   // F of the last solve
-  std::vector<double> packed_;  // F being packed
-  bool solved_ = false;         // the engine holds T of speed_ for the goal below
+  double* dF_ = nullptr;
+  double* dT_ = nullptr;
+  uint64_t dcells_ = 0;
+  // host mirror of dT_
+  mutable std::vector<double> total_cost_;
+  mutable std::vector<uint8_t> blk_ok_;
+  mutable uint64_t blk_missing_ = 0;
+  unsigned nbx_ = 0, nby_ = 0;
+  void* registered_ = nullptr;  // total_cost_ buffer page-locked for DMA
+  double closed_limit_ = 0.0;   // CLOSED iff finite T <= closed_limit_
+  uint64_t band_size_ = 0;
+  // F as uploaded to dF_ (host copy); node-field rows [dirty_j0_, dirty_j1_)
+  // changed since it was packed
+  std::vector<double> speed_;
+  std::vector<double> row_;
+  bool speed_valid_ = false;
+  unsigned dirty_j0_ = 0, dirty_j1_ = 0;
+  bool solved_ = false;  // dT_ holds the converged map of speed_ for the goal below
   unsigned solved_gi_ = 0, solved_gj_ = 0;
   int incremental_ = 0;  // last solve: 0 cold, 1 windowed re-propagation, 2 reused
 };

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DYMU_ABI_VERSION 2
+#define DYMU_ABI_VERSION 3
 
 typedef enum dymu_status {
   DYMU_OK = 0,
@@ -97,6 +97,36 @@ int dymu_solve(dymu_ctx* ctx, const double* F, uint32_t nx, uint32_t ny, uint32_
 int dymu_solve_device(dymu_ctx* ctx, const double* dF, double* dT, uint32_t nx, uint32_t ny,
                       uint64_t ld, uint32_t goal_i, uint32_t goal_j, void* stream,
                       dymu_stats* stats);
+
+/* ---- computeTotalCostMap's early exit (reference src/DyMu_GlobalPathPlanning.cpp:364-408) ----
+ * The reference stops its FMM as soon as the start node and its 4-neighbours
+ * are CLOSED (isFullyClosedNode :424-436).  dymu_solve_until_device is
+ * dymu_solve_device with that stop: it returns as soon as every queued tile's
+ * priority key -- a lower bound on any value the remaining passes can produce --
+ * exceeds t = max T over the start (start_i, start_j) and its in-grid
+ * 4-neighbours, or when the map has converged.  On return every cell whose
+ * converged value is <= *t_closed = t holds that value (the reference's CLOSED
+ * set); other cells hold upper bounds.  *t_closed = +inf when the start is
+ * unreachable (the whole map is then converged).  Runs a priority kernel (4 or
+ * 5) whatever dymu_opts.kernel says. */
+int dymu_solve_until_device(dymu_ctx* ctx, const double* dF, double* dT, uint32_t nx,
+                            uint32_t ny, uint64_t ld, uint32_t goal_i, uint32_t goal_j,
+                            uint32_t start_i, uint32_t start_j, void* stream, double* t_closed,
+                            dymu_stats* stats);
+/* The node states after that early exit: a cell is CLOSED iff T <= t_closed and
+ * keeps T; a finite-speed 4-neighbour of a CLOSED cell is in the narrow band
+ * (the reference propagated into it, :462-465) and keeps its current T for the
+ * caller to replace with the reference's tentative value; every other cell
+ * gets +inf (never reached: -1 in getTotalCostMatrix).  band_idx: host buffer
+ * of `cap` entries receiving the band cells' indices j*nx + i (unordered);
+ * *n_band = their number -- if it exceeds cap only cap were written, and the
+ * call may be repeated with a larger buffer (it is idempotent). */
+int dymu_early_exit_mask(dymu_ctx* ctx, const double* dF, double* dT, uint32_t nx, uint32_t ny,
+                         uint64_t ld, double t_closed, uint64_t* band_idx, uint64_t cap,
+                         uint64_t* n_band, void* stream);
+/* dT[(idx[k] / nx) * ld + idx[k] % nx] = vals[k] for k < n (idx, vals: host). */
+int dymu_scatter(dymu_ctx* ctx, double* dT, uint32_t nx, uint64_t ld, const uint64_t* idx,
+                 const double* vals, uint64_t n, void* stream);
 
 /* ---- row-slab domains (multi-GPU sharding; also single-GPU virtual slabs) ----
  * A rank owns rows [row0, row0+nrows) of an nx-wide global grid.  T points at
@@ -164,6 +194,14 @@ int dymu_device_alloc(dymu_ctx* ctx, size_t bytes, void** dptr);
 int dymu_device_free(dymu_ctx* ctx, void* dptr);
 int dymu_memcpy_d2h(dymu_ctx* ctx, void* dst, const void* src, size_t bytes);
 int dymu_memcpy_h2d(dymu_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* pitched copies (hipMemcpy2D: width bytes per row, height rows) */
+int dymu_memcpy2d_d2h(dymu_ctx* ctx, void* dst, size_t dpitch, const void* src, size_t spitch,
+                      size_t width, size_t height);
+int dymu_memcpy2d_h2d(dymu_ctx* ctx, void* dst, size_t dpitch, const void* src, size_t spitch,
+                      size_t width, size_t height);
+/* page-lock a host buffer for full-speed DMA (hipHostRegister) / undo it */
+int dymu_host_register(dymu_ctx* ctx, void* p, size_t bytes);
+int dymu_host_unregister(dymu_ctx* ctx, void* p);
 
 /* ---- dynamic update: windowed re-propagation ----
  * After the speed changed only inside the window [i0, i0+w) x [j0, j0+h)

@@ -62,6 +62,9 @@ struct dymu_ctx {
   unsigned long long* d_prio = nullptr;
   uint32_t epoch_base = 0;
   uint32_t* h_count = nullptr;  // pinned
+  unsigned long long* h_probe = nullptr;  // pinned [2]: early-exit probe (max T, min key)
+  uint64_t* d_band = nullptr;   // early-exit band indices (device)
+  uint64_t band_cap = 0;
   unsigned long long* d_scratch = nullptr;  // 8 words of per-call device scalars
   double* d_lut = nullptr;      // computeCostMap LUT (device copy)
   size_t lut_cap = 0;
@@ -187,9 +190,12 @@ void dom_retire(dymu_ctx* c) {
 // ---- domain primitives (whole grid, or one row slab with ghost rows) ----
 // cold = true: T := +inf (incl. ghost rows) and the goal seeded (a fresh solve);
 // false: T is kept and the caller seeds list 0 (windowed re-propagation).
+// need_keys: the caller needs tile keys (lower bounds on every value the passes can
+// still produce, dymu_solve_until_device): the plain FIM kernel 3 has none, kernel 4
+// runs instead.
 int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t nrows, uint64_t ld,
               int ghost_lo, int ghost_hi, int64_t gi, int64_t gj, hipStream_t st,
-              bool cold = true) {
+              bool cold = true, bool need_keys = false) {
   if (!dF || !dT || nx == 0 || nrows == 0 || ld < nx) return DYMU_ERR_ARG;
   int variant = c->variant;
   if (variant == 0) {
@@ -197,6 +203,7 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
                         (uint64_t)((nrows + kWaveTile - 1) / kWaveTile);
     variant = t8 >= c->prio_min_tiles ? 5 : 3;
   }
+  if (need_keys && !is_prio(variant)) variant = 4;
   const int TWd = tile_w(variant), THd = tile_h(variant);
   if (ghost_hi && (nrows % (uint32_t)THd) != 0) return DYMU_ERR_ARG;
   if (gj >= 0 && (gi < 0 || gi >= (int64_t)nx || gj >= (int64_t)nrows)) return DYMU_ERR_ARG;
@@ -465,15 +472,38 @@ int dom_finish(dymu_ctx* c, hipStream_t st, dymu_stats* stats, double ms) {
   return DYMU_OK;
 }
 
-// passes until no tile is queued, then statistics (the domain must be live)
-int converge(dymu_ctx* c, hipStream_t st, dymu_stats* stats) {
+// passes until no tile is queued, then statistics (the domain must be live).
+// probe (priority kernels only): also stop as soon as the probe cells are final --
+// every queued tile's key exceeds their largest value -- and return that value in
+// *t_probe (+inf if a probe cell is unreachable; then the solve runs to the end).
+int converge(dymu_ctx* c, hipStream_t st, dymu_stats* stats, const ProbeCells* probe = nullptr,
+             double* t_probe = nullptr) {
   HIPC(c, hipEventRecord(c->ev0, st));
   uint64_t K = c->opts.passes_per_check > 0 ? (uint64_t)c->opts.passes_per_check : c->first_batch;
   for (;;) {
     int rc = dom_launch(c, K, st);
+    if (rc == DYMU_OK && probe) {
+      auto& D = c->dom;
+      const hipError_t e = launch_probe(D.a.T, D.a.ld, *probe, prio_minkey(c, D.p % 3),
+                                        c->d_scratch + 2, st);
+      rc = e == hipSuccess ? DYMU_OK : fail_hip(c, e, "launch_probe");
+      if (rc == DYMU_OK) {
+        const hipError_t e2 = hipMemcpyAsync(c->h_probe, c->d_scratch + 2,
+                                             2 * sizeof(unsigned long long),
+                                             hipMemcpyDeviceToHost, st);
+        if (e2 != hipSuccess) rc = fail_hip(c, e2, "probe read-back");
+      }
+    }
     if (rc == DYMU_OK) {
       uint64_t pending = 0;
       rc = dom_pending(c, st, &pending);
+      if (rc == DYMU_OK && probe) {
+        double tmax, kmin;
+        std::memcpy(&tmax, &c->h_probe[0], sizeof tmax);
+        std::memcpy(&kmin, &c->h_probe[1], sizeof kmin);
+        *t_probe = tmax;
+        if (kmin > tmax) break;  // no pass can lower a value <= tmax any more
+      }
       if (rc == DYMU_OK && pending == 0) break;
     }
     if (rc == DYMU_OK && c->dom.p >= c->dom.max_passes) {
@@ -499,6 +529,35 @@ int solve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t 
   int rc = dom_begin(c, dF, dT, nx, ny, ld, 0, 0, gi, gj, st);
   if (rc) return rc;
   return converge(c, st, stats);
+}
+
+// The start cell and its in-grid 4-neighbours (isFullyClosedNode, :424-436).
+ProbeCells start_probe(uint32_t nx, uint32_t ny, uint32_t si, uint32_t sj) {
+  ProbeCells p{};
+  auto add = [&](int64_t i, int64_t j) {
+    if (i >= 0 && j >= 0 && i < (int64_t)nx && j < (int64_t)ny) {
+      p.ij[p.n][0] = i;
+      p.ij[p.n][1] = j;
+      ++p.n;
+    }
+  };
+  add(si, sj);
+  add(si, (int64_t)sj - 1);
+  add((int64_t)si - 1, sj);
+  add((int64_t)si + 1, sj);
+  add(si, (int64_t)sj + 1);
+  return p;
+}
+
+int solve_until_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t ny,
+                     uint64_t ld, uint32_t gi, uint32_t gj, uint32_t si, uint32_t sj,
+                     hipStream_t st, double* t_closed, dymu_stats* stats) {
+  if (gi >= nx || gj >= ny || si >= nx || sj >= ny || !t_closed) return DYMU_ERR_ARG;
+  int rc = dom_begin(c, dF, dT, nx, ny, ld, 0, 0, gi, gj, st, true, /*need_keys=*/true);
+  if (rc) return rc;
+  const ProbeCells p = start_probe(nx, ny, si, sj);
+  *t_closed = __builtin_inf();
+  return converge(c, st, stats, &p, t_closed);
 }
 
 // Windowed re-propagation (update_kernels.hip): dT holds the converged map of
@@ -636,6 +695,8 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
   if (e == hipSuccess)
     e = hipMalloc(&c->d_stats, sizeof(unsigned long long) * kShards * kStatSlots);
   if (e == hipSuccess) e = hipHostMalloc(&c->h_count, sizeof(uint32_t) * 4 * kShards, hipHostMallocDefault);
+  if (e == hipSuccess)
+    e = hipHostMalloc(&c->h_probe, sizeof(unsigned long long) * 2, hipHostMallocDefault);
   if (e != hipSuccess) {
     dymu_destroy(c);
     return e == hipErrorOutOfMemory ? DYMU_ERR_NOMEM : DYMU_ERR_HIP;
@@ -665,6 +726,8 @@ int dymu_destroy(dymu_ctx* c) {
   if (c->d_F) (void)hipFree(c->d_F);
   if (c->d_T) (void)hipFree(c->d_T);
   if (c->h_count) (void)hipHostFree(c->h_count);
+  if (c->h_probe) (void)hipHostFree(c->h_probe);
+  if (c->d_band) (void)hipFree(c->d_band);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return DYMU_OK;
@@ -695,6 +758,94 @@ int dymu_solve(dymu_ctx* c, const double* F, uint32_t nx, uint32_t ny, uint32_t 
   c->host_ny = ny;
   c->host_gi = gi;
   c->host_gj = gj;
+  return DYMU_OK;
+}
+
+int dymu_solve_until_device(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t ny,
+                            uint64_t ld, uint32_t gi, uint32_t gj, uint32_t si, uint32_t sj,
+                            void* stream, double* t_closed, dymu_stats* stats) {
+  if (!c) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  return solve_until_core(c, dF, dT, nx, ny, ld, gi, gj, si, sj, pick_stream(c, stream), t_closed,
+                          stats);
+}
+
+int dymu_early_exit_mask(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t ny,
+                         uint64_t ld, double t_closed, uint64_t* band_idx, uint64_t cap,
+                         uint64_t* n_band, void* stream) {
+  if (!c || !dF || !dT || !n_band || nx == 0 || ny == 0 || ld < nx || (cap && !band_idx))
+    return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  hipStream_t st = pick_stream(c, stream);
+  if (cap > c->band_cap) {
+    if (c->d_band) HIPC(c, hipFree(c->d_band));
+    c->d_band = nullptr;
+    c->band_cap = 0;
+    HIPC(c, hipMalloc(&c->d_band, sizeof(uint64_t) * cap));
+    c->band_cap = cap;
+  }
+  unsigned long long* cnt = c->d_scratch + 4;
+  HIPC(c, hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
+  HIPC(c, launch_early_mask(dF, dT, (int64_t)ld, nx, ny, t_closed, c->d_band, cnt, cap, st));
+  HIPC(c, hipMemcpyAsync(c->h_probe, cnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  HIPC(c, hipStreamSynchronize(st));
+  *n_band = c->h_probe[0];
+  const uint64_t m = std::min<uint64_t>(*n_band, cap);
+  if (m) HIPC(c, hipMemcpy(band_idx, c->d_band, sizeof(uint64_t) * m, hipMemcpyDeviceToHost));
+  return DYMU_OK;
+}
+
+int dymu_scatter(dymu_ctx* c, double* dT, uint32_t nx, uint64_t ld, const uint64_t* idx,
+                 const double* vals, uint64_t n, void* stream) {
+  if (!c || !dT || nx == 0 || ld < nx || (n && (!idx || !vals))) return DYMU_ERR_ARG;
+  if (n == 0) return DYMU_OK;
+  HIPC(c, hipSetDevice(c->device));
+  hipStream_t st = pick_stream(c, stream);
+  uint64_t* di = nullptr;
+  double* dv = nullptr;
+  HIPC(c, hipMallocAsync(reinterpret_cast<void**>(&di), sizeof(uint64_t) * n, st));
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&dv), sizeof(double) * n, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(di, idx, sizeof(uint64_t) * n, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dv, vals, sizeof(double) * n, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = launch_scatter(dT, (int64_t)ld, nx, di, dv, n, st);
+  if (dv) (void)hipFreeAsync(dv, st);
+  (void)hipFreeAsync(di, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return fail_hip(c, e, "dymu_scatter");
+  return DYMU_OK;
+}
+
+int dymu_memcpy2d_d2h(dymu_ctx* c, void* dst, size_t dpitch, const void* src, size_t spitch,
+                      size_t width, size_t height) {
+  if (!c || !dst || !src) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  HIPC(c, hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToHost,
+                           c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return DYMU_OK;
+}
+
+int dymu_memcpy2d_h2d(dymu_ctx* c, void* dst, size_t dpitch, const void* src, size_t spitch,
+                      size_t width, size_t height) {
+  if (!c || !dst || !src) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  HIPC(c, hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyHostToDevice,
+                           c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return DYMU_OK;
+}
+
+int dymu_host_register(dymu_ctx* c, void* p, size_t bytes) {
+  if (!c || !p || bytes == 0) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  HIPC(c, hipHostRegister(p, bytes, hipHostRegisterDefault));
+  return DYMU_OK;
+}
+
+int dymu_host_unregister(dymu_ctx* c, void* p) {
+  if (!c || !p) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  HIPC(c, hipHostUnregister(p));
   return DYMU_OK;
 }
 

@@ -135,6 +135,24 @@ hipError_t launch_reset_seed(const UpdateArgs& a, hipStream_t st);
 hipError_t launch_theta_state(const unsigned long long* theta_bits, unsigned long long* minkey0,
                               double* base0, hipStream_t st);
 
+// early exit of computeTotalCostMap (update_kernels.hip)
+struct ProbeCells {
+  int64_t ij[5][2];  // (i, j) of the start cell and its in-grid 4-neighbours
+  int n;
+};
+// out[0] = bits of max T over the probe cells, out[1] = *minkey (or +inf bits if null)
+hipError_t launch_probe(const double* T, int64_t ld, const ProbeCells& cells,
+                        const unsigned long long* minkey, unsigned long long* out,
+                        hipStream_t st);
+// reference node states after the early exit: T > t_closed -> +inf unless the cell is a
+// finite-speed 4-neighbour of a cell with T <= t_closed (the band: index appended to band)
+hipError_t launch_early_mask(const double* F, double* T, int64_t ld, uint32_t nx, uint32_t ny,
+                             double t_closed, uint64_t* band, unsigned long long* n_band,
+                             uint64_t cap, hipStream_t st);
+// T[(idx / nx) * ld + idx % nx] = vals[k]
+hipError_t launch_scatter(double* T, int64_t ld, uint32_t nx, const uint64_t* idx,
+                          const double* vals, uint64_t n, hipStream_t st);
+
 hipError_t launch_prio_init(const double* F, int64_t ld, int64_t nx, int64_t ny,
                            unsigned long long* keys, uint64_t nkeys, uint32_t* hist, uint64_t nhist,
                            unsigned long long* minkey, double* base, double* delta, double kappa,

@@ -4,7 +4,12 @@
 // path extraction run on the host exactly as the reference computes them
 // (compiled with -ffp-contract=off so each operation rounds where the
 // reference's does); the total-cost propagation -- the reference's FMM loop
-// -- is one dymu_solve() call on the GPU.
+// -- runs on the GPU over a device-resident speed / total-cost map:
+//   * the speed F is packed on the host only for the rows whose node fields
+//     changed, and only the rows whose speed changed are uploaded;
+//   * the total cost stays on the device; the host mirror fetches blocks of it
+//     on first read (path extraction reads a narrow band around the path) or
+//     all of it for the matrix getters.
 #include <algorithm>
 #include <cstring>
 #include <cmath>
@@ -12,6 +17,7 @@
 #include <limits>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 
 #include "DyMu.hpp"
 
@@ -31,16 +37,30 @@ DyMuPathPlanner::DyMuPathPlanner(double risk_distance, double reconnect_distance
       risk_ratio_(risk_ratio),
       repairing_approach_(input_approach) {}
 
+namespace {
+void release_engine(dymu_ctx*& ctx, double*& dF, double*& dT, void*& reg, uint64_t& cells) {
+  if (!ctx) return;
+  if (reg) (void)dymu_host_unregister(ctx, reg);
+  if (dF) (void)dymu_device_free(ctx, dF);
+  if (dT) (void)dymu_device_free(ctx, dT);
+  dymu_destroy(ctx);
+  ctx = nullptr;
+  dF = dT = nullptr;
+  reg = nullptr;
+  cells = 0;
+}
+}  // namespace
+
 DyMuPathPlanner::~DyMuPathPlanner() {
-  if (ctx_) dymu_destroy(ctx_);
+  release_engine(ctx_, dF_, dT_, registered_, dcells_);
 }
 
 void DyMuPathPlanner::setEngineOptions(const dymu_opts& o) {
   opts_ = o;
-  if (ctx_) {
-    dymu_destroy(ctx_);
-    ctx_ = nullptr;
-  }
+  release_engine(ctx_, dF_, dT_, registered_, dcells_);
+  solved_ = false;
+  speed_valid_ = false;
+  markDirty(0, ny_);
 }
 
 // :39-104.  Node fields start as the globalNode constructor sets them
@@ -63,13 +83,24 @@ bool DyMuPathPlanner::initGlobalLayer(double globalres, double localres, unsigne
   cost_.assign(n, 0.0);
   hazard_.assign(n, 0.0);
   traff_.assign(n, 1.0);
-  total_cost_.assign(n, kInf);
   terrain_.assign(n, 0u);
   is_obstacle_.assign(n, 0);
-  state_.assign(n, OPEN);
   loc_mode_.assign(n, -1);
   has_goal_ = false;
   current_path.clear();
+  // a new grid: new device buffers and an empty total-cost map (every node
+  // OPEN at +inf, as the globalNode constructor leaves it)
+  release_engine(ctx_, dF_, dT_, registered_, dcells_);
+  total_cost_.assign(n, kInf);
+  nbx_ = (nx_ + kBlk - 1) / kBlk;
+  nby_ = (ny_ + kBlk - 1) / kBlk;
+  blk_ok_.assign((uint64_t)nbx_ * nby_, 1);
+  blk_missing_ = 0;
+  closed_limit_ = 0.0;
+  band_size_ = 0;
+  speed_.clear();
+  speed_valid_ = false;
+  markDirty(0, ny_);
   return true;
 }
 
@@ -89,6 +120,7 @@ bool DyMuPathPlanner::setCostMap(std::vector<std::vector<double>> cost_map) {
       }
     }
   }
+  markDirty(0, ny_);
   return true;
 }
 
@@ -195,6 +227,7 @@ bool DyMuPathPlanner::computeCostMap(std::vector<double> cost_data,
       if (j == ny_ - 1) n--; else csum += raw_cost_[k + nx_];
       cost_[k] = csum / n;
     }
+  markDirty(0, ny_);
   return true;
 }
 
@@ -217,30 +250,75 @@ bool DyMuPathPlanner::setGoal(base::Waypoint wGoal) {
   return true;
 }
 
+namespace {
+// rows of a vs b (ny rows of nx) that differ: [*j0, *j1), empty if none
+void diff_rows(const double* a, const double* b, unsigned nx, unsigned ny, unsigned* j0,
+               unsigned* j1) {
+  *j0 = ny;
+  *j1 = 0;
+  for (unsigned j = 0; j < ny; ++j)
+    if (std::memcmp(a + (uint64_t)j * nx, b + (uint64_t)j * nx, sizeof(double) * nx) != 0) {
+      if (*j0 == ny) *j0 = j;
+      *j1 = j + 1;
+    }
+}
+}  // namespace
+
+void DyMuPathPlanner::markDirty(unsigned j0, unsigned j1) {
+  if (j0 >= j1) return;
+  if (dirty_j0_ >= dirty_j1_) {
+    dirty_j0_ = j0;
+    dirty_j1_ = j1;
+  } else {
+    dirty_j0_ = std::min(dirty_j0_, j0);
+    dirty_j1_ = std::max(dirty_j1_, j1);
+  }
+}
+
 bool DyMuPathPlanner::setHazardDensity(const std::vector<double>& hd) {
   if (hd.size() != hazard_.size()) return false;
-  hazard_ = hd;
+  unsigned j0, j1;
+  diff_rows(hd.data(), hazard_.data(), nx_, ny_, &j0, &j1);
+  if (j0 < j1) {
+    std::memcpy(&hazard_[idx(0, j0)], &hd[idx(0, j0)], sizeof(double) * (uint64_t)(j1 - j0) * nx_);
+    markDirty(j0, j1);
+  }
   return true;
 }
 
 bool DyMuPathPlanner::setTrafficability(const std::vector<double>& tr) {
   if (tr.size() != traff_.size()) return false;
-  traff_ = tr;
+  unsigned j0, j1;
+  diff_rows(tr.data(), traff_.data(), nx_, ny_, &j0, &j1);
+  if (j0 < j1) {
+    std::memcpy(&traff_[idx(0, j0)], &tr[idx(0, j0)], sizeof(double) * (uint64_t)(j1 - j0) * nx_);
+    markDirty(j0, j1);
+  }
   return true;
 }
 
-// The engine call: F = global_res * cost * (2 + hazard - traff) (:527-528),
-// +inf for obstacles; T and node states come back for every cell.
-// Incremental path: when the previous solve on this engine was
-// of the same grid and goal and the speed changed only inside a window (the
-// local layer's hazard / trafficability writes), the engine re-propagates
-// from that window (dymu_resolve_window) instead of solving cold; unchanged
-// speed reuses the previous map.  Both give the cold solve's fixed point.
-bool DyMuPathPlanner::solveFull() {
+bool DyMuPathPlanner::setHazardDensityWindow(unsigned i0, unsigned j0, unsigned w, unsigned h,
+                                             const double* hd) {
+  if (!hd || (uint64_t)i0 + w > nx_ || (uint64_t)j0 + h > ny_) return false;
+  for (unsigned r = 0; r < h; ++r)
+    std::memcpy(&hazard_[idx(i0, j0 + r)], hd + (uint64_t)r * w, sizeof(double) * w);
+  markDirty(j0, j0 + h);
+  return true;
+}
+
+bool DyMuPathPlanner::setTrafficabilityWindow(unsigned i0, unsigned j0, unsigned w, unsigned h,
+                                              const double* tr) {
+  if (!tr || (uint64_t)i0 + w > nx_ || (uint64_t)j0 + h > ny_) return false;
+  for (unsigned r = 0; r < h; ++r)
+    std::memcpy(&traff_[idx(i0, j0 + r)], tr + (uint64_t)r * w, sizeof(double) * w);
+  markDirty(j0, j0 + h);
+  return true;
+}
+
+// ---- the device-resident map ----
+
+void DyMuPathPlanner::ensureEngine() {
   const uint64_t n = (uint64_t)nx_ * ny_;
-  packed_.resize(n);
-  for (uint64_t k = 0; k < n; ++k)
-    packed_[k] = is_obstacle_[k] ? kInf : global_res_ * cost_[k] * (2 + hazard_[k] - traff_[k]);
   if (!ctx_) {
     const int rc = dymu_create(&ctx_, &opts_);
     if (rc != DYMU_OK) {
@@ -249,47 +327,270 @@ bool DyMuPathPlanner::solveFull() {
                                dymu_strerror(rc));
     }
     solved_ = false;
+    speed_valid_ = false;
   }
-  int rc = DYMU_ERR_STATE;
-  if (solved_ && speed_.size() == n && solved_gi_ == goal_i_ && solved_gj_ == goal_j_) {
-    // bounding box of the cells whose speed changed (bitwise)
-    unsigned i0 = nx_, i1 = 0, j0 = ny_, j1 = 0;
-    for (unsigned j = 0; j < ny_; ++j) {
-      const double* a = &packed_[idx(0, j)];
-      const double* b = &speed_[idx(0, j)];
-      if (std::memcmp(a, b, sizeof(double) * nx_) == 0) continue;
-      for (unsigned i = 0; i < nx_; ++i)
-        if (std::memcmp(a + i, b + i, sizeof(double)) != 0) {
-          i0 = std::min(i0, i);
-          i1 = std::max(i1, i + 1);
-        }
-      j0 = std::min(j0, j);
-      j1 = j + 1;
+  if (dcells_ != n) {
+    if (dF_) (void)dymu_device_free(ctx_, dF_);
+    if (dT_) (void)dymu_device_free(ctx_, dT_);
+    dF_ = dT_ = nullptr;
+    dcells_ = 0;
+    void *f = nullptr, *t = nullptr;
+    if (dymu_device_alloc(ctx_, sizeof(double) * n, &f) != DYMU_OK ||
+        dymu_device_alloc(ctx_, sizeof(double) * n, &t) != DYMU_OK) {
+      if (f) (void)dymu_device_free(ctx_, f);
+      throw std::runtime_error("dymu: cannot allocate the device map");
     }
-    if (i1 == 0) {  // nothing changed: the map stands
+    dF_ = static_cast<double*>(f);
+    dT_ = static_cast<double*>(t);
+    dcells_ = n;
+    solved_ = false;
+    speed_valid_ = false;
+    // page-lock the host mirror for full-rate downloads (optional: pageable works)
+    if (registered_) (void)dymu_host_unregister(ctx_, registered_);
+    registered_ = nullptr;
+    if (dymu_host_register(ctx_, total_cost_.data(), sizeof(double) * n) == DYMU_OK)
+      registered_ = total_cost_.data();
+  }
+  if (!speed_valid_) {
+    speed_.assign(n, 0.0);
+    markDirty(0, ny_);
+  }
+}
+
+// F = global_res * cost * (2 + hazard - traff) (:527-528), +inf for obstacles,
+// re-packed for the dirty rows; the rows whose F changed are uploaded.
+bool DyMuPathPlanner::syncSpeed(unsigned& i0, unsigned& i1, unsigned& j0, unsigned& j1) {
+  i0 = nx_;
+  i1 = 0;
+  j0 = ny_;
+  j1 = 0;
+  if (dirty_j0_ >= dirty_j1_ && speed_valid_) return false;
+  const unsigned d0 = speed_valid_ ? dirty_j0_ : 0, d1 = speed_valid_ ? dirty_j1_ : ny_;
+  row_.resize(nx_);
+  for (unsigned j = d0; j < d1; ++j) {
+    const uint64_t k0 = idx(0, j);
+    for (unsigned i = 0; i < nx_; ++i) {
+      const uint64_t k = k0 + i;
+      row_[i] = is_obstacle_[k] ? kInf : global_res_ * cost_[k] * (2 + hazard_[k] - traff_[k]);
+    }
+    double* old = &speed_[k0];
+    if (speed_valid_ && std::memcmp(row_.data(), old, sizeof(double) * nx_) == 0) continue;
+    unsigned a = 0, b = nx_;
+    if (speed_valid_) {
+      while (std::memcmp(&row_[a], old + a, sizeof(double)) == 0) ++a;
+      while (std::memcmp(&row_[b - 1], old + b - 1, sizeof(double)) == 0) --b;
+    }
+    std::memcpy(old, row_.data(), sizeof(double) * nx_);
+    i0 = std::min(i0, a);
+    i1 = std::max(i1, b);
+    if (j0 == ny_) j0 = j;
+    j1 = j + 1;
+  }
+  dirty_j0_ = dirty_j1_ = 0;
+  if (!speed_valid_) {
+    i0 = 0, i1 = nx_, j0 = 0, j1 = ny_;
+  }
+  speed_valid_ = true;
+  if (j0 >= j1) return false;
+  const int rc = dymu_memcpy_h2d(ctx_, dF_ + idx(0, j0), &speed_[idx(0, j0)],
+                                 sizeof(double) * (uint64_t)(j1 - j0) * nx_);
+  if (rc != DYMU_OK) {
+    speed_valid_ = false;
+    throw std::runtime_error(std::string("dymu: speed upload failed: ") + dymu_last_error(ctx_));
+  }
+  return true;
+}
+
+double DyMuPathPlanner::T(uint64_t k) const {
+  if (blk_missing_) {
+    const unsigned j = (unsigned)(k / nx_), i = (unsigned)(k % nx_);
+    const uint64_t b = (uint64_t)(j / kBlk) * nbx_ + i / kBlk;
+    if (!blk_ok_[b]) {
+      const unsigned bi = (i / kBlk) * kBlk, bj = (j / kBlk) * kBlk;
+      const unsigned w = std::min(kBlk, nx_ - bi), h = std::min(kBlk, ny_ - bj);
+      const uint64_t o = idx(bi, bj);
+      if (dymu_memcpy2d_d2h(ctx_, &total_cost_[o], sizeof(double) * nx_, dT_ + o,
+                            sizeof(double) * nx_, sizeof(double) * w, h) != DYMU_OK)
+        throw std::runtime_error(std::string("dymu: total-cost download failed: ") +
+                                 dymu_last_error(ctx_));
+      blk_ok_[b] = 1;
+      --blk_missing_;
+    }
+  }
+  return total_cost_[k];
+}
+
+void DyMuPathPlanner::fetchAll() const {
+  if (!blk_missing_) return;
+  if (dymu_memcpy_d2h(ctx_, total_cost_.data(), dT_, sizeof(double) * dcells_) != DYMU_OK)
+    throw std::runtime_error(std::string("dymu: total-cost download failed: ") +
+                             dymu_last_error(ctx_));
+  std::fill(blk_ok_.begin(), blk_ok_.end(), 1);
+  blk_missing_ = 0;
+}
+
+const double* DyMuPathPlanner::totalCostData() const {
+  fetchAll();
+  return total_cost_.data();
+}
+
+bool DyMuPathPlanner::closedCell(uint64_t k) const {
+  const double t = T(k);
+  return t < kInf && t <= closed_limit_;
+}
+
+// One propagation on the engine.  early = computeTotalCostMap (:364-408): stop
+// once (si, sj) and its nb4 are final, then rebuild the reference's node states
+// (CLOSED / band / never reached) and the band's tentative values.  Otherwise
+// computeEntireTotalCostMap (:443-468), incremental where possible: when dT_
+// holds the converged map of the same grid and goal and the speed changed only
+// inside a window (the local layer's hazard / trafficability writes), the engine
+// re-propagates from that window (dymu_resolve_window_device); unchanged speed
+// reuses the map.  Both give the cold solve's fixed point.
+// Returns false iff the early exit left an empty band (the reference's "goal
+// unreachable" return, :399-403).
+bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
+  ensureEngine();
+  unsigned i0, i1, j0, j1;
+  const bool changed = syncSpeed(i0, i1, j0, j1);
+  const uint64_t n = (uint64_t)nx_ * ny_;
+  int rc = DYMU_ERR_STATE;
+  if (!early && solved_ && solved_gi_ == goal_i_ && solved_gj_ == goal_j_) {
+    if (!changed) {
       incremental_ = 2;
       return true;
     }
-    if ((uint64_t)(i1 - i0) * (j1 - j0) * 4 <= n) {  // a window: re-propagate from it
-      rc = dymu_resolve_window(ctx_, packed_.data(), nx_, ny_, goal_i_, goal_j_, i0, j0, i1 - i0,
-                               j1 - j0, total_cost_.data(), &stats_);
+    if ((uint64_t)(i1 - i0) * (j1 - j0) * 4 <= n) {
+      rc = dymu_resolve_window_device(ctx_, dF_, dT_, nx_, ny_, nx_, goal_i_, goal_j_, i0, j0,
+                                      i1 - i0, j1 - j0, nullptr, &stats_);
       if (rc == DYMU_OK) incremental_ = 1;
     }
   }
+  double t_closed = kInf;
   if (rc != DYMU_OK) {
     solved_ = false;
-    rc = dymu_solve(ctx_, packed_.data(), nx_, ny_, goal_i_, goal_j_, total_cost_.data(), &stats_);
+    rc = early ? dymu_solve_until_device(ctx_, dF_, dT_, nx_, ny_, nx_, goal_i_, goal_j_, si, sj,
+                                         nullptr, &t_closed, &stats_)
+               : dymu_solve_device(ctx_, dF_, dT_, nx_, ny_, nx_, goal_i_, goal_j_, nullptr,
+                                   &stats_);
     if (rc != DYMU_OK)
-      throw std::runtime_error(std::string("dymu_solve failed: ") + dymu_strerror(rc) + " " +
+      throw std::runtime_error(std::string("dymu solve failed: ") + dymu_strerror(rc) + " " +
                                dymu_last_error(ctx_));
     incremental_ = 0;
   }
-  speed_.swap(packed_);
-  solved_ = true;
-  solved_gi_ = goal_i_;
-  solved_gj_ = goal_j_;
-  for (uint64_t k = 0; k < n; ++k) state_[k] = total_cost_[k] < kInf ? CLOSED : OPEN;
-  return true;
+  // the host mirror is stale
+  std::fill(blk_ok_.begin(), blk_ok_.end(), 0);
+  blk_missing_ = blk_ok_.size();
+  band_size_ = 0;
+  if (!early) {
+    closed_limit_ = kInf;
+    solved_ = true;
+    solved_gi_ = goal_i_;
+    solved_gj_ = goal_j_;
+    return true;
+  }
+  // early exit: the reference's CLOSED set is {T <= t_closed}; the band gets its
+  // tentative values; every other cell +inf.  dT_ is no longer a converged map.
+  solved_ = false;
+  closed_limit_ = t_closed;
+  std::vector<uint64_t> band(std::max<uint64_t>(4096, 4 * (uint64_t)(nx_ + ny_)));
+  uint64_t nb = 0;
+  for (;;) {
+    rc = dymu_early_exit_mask(ctx_, dF_, dT_, nx_, ny_, nx_, t_closed, band.data(), band.size(),
+                              &nb, nullptr);
+    if (rc != DYMU_OK)
+      throw std::runtime_error(std::string("dymu_early_exit_mask failed: ") +
+                               dymu_last_error(ctx_));
+    if (nb <= band.size()) break;
+    band.resize(nb);
+  }
+  band.resize(nb);
+  std::sort(band.begin(), band.end());
+  band_size_ = nb;
+  if (nb) {
+    std::vector<double> vals;
+    replayBand(t_closed, band, vals);
+    rc = dymu_scatter(ctx_, dT_, nx_, nx_, band.data(), vals.data(), nb, nullptr);
+    if (rc != DYMU_OK)
+      throw std::runtime_error(std::string("dymu_scatter failed: ") + dymu_last_error(ctx_));
+    // blocks fetched during the replay hold the pre-replay band values
+    for (uint64_t q = 0; q < nb; ++q) total_cost_[band[q]] = vals[q];
+  }
+  return nb > 0;
+}
+
+// The reference's tentative band values at its early exit, from the CLOSED
+// values.  FMM pops in increasing T (the CLOSED cells, T <= t_closed, are popped
+// in the order of their values), and each pop of a node c updates its OPEN
+// nb4 x from the values x's neighbours hold at that moment (:462-465, :500-546).
+// So x's value just after all pops up to time t is
+//   val(x, t) = min over CLOSED nb4 c of x with T(c) <= t of cand(x, T(c)),
+// where cand(x, te) is the update with each neighbour n at its value at te: T(n)
+// if n is CLOSED with T(n) <= te, else val(n, te) (n is OPEN then; no pop at te
+// other than c touches n: the grid is bipartite).  An OPEN value at te is >= te
+// >= any CLOSED value at te (the FMM invariant), so an axis with a CLOSED side
+// takes that side and recursion only follows axes whose both sides are OPEN --
+// cells next to the front, at strictly earlier pops.  Ties between equal T
+// values (the reference's insertion order) are not reproduced.
+void DyMuPathPlanner::replayBand(double t_closed, const std::vector<uint64_t>& band,
+                                 std::vector<double>& out) {
+  struct KeyHash {
+    size_t operator()(const std::pair<uint64_t, double>& k) const {
+      uint64_t b;
+      std::memcpy(&b, &k.second, sizeof b);
+      return std::hash<uint64_t>()(k.first * 0x9E3779B97F4A7C15ull ^ b);
+    }
+  };
+  struct Replay {
+    const DyMuPathPlanner& pl;
+    const double* F;
+    double t_closed;
+    int64_t NX, NY;
+    std::unordered_map<std::pair<uint64_t, double>, double, KeyHash> memo;
+
+    bool in_grid(int64_t i, int64_t j) const { return i >= 0 && j >= 0 && i < NX && j < NY; }
+    // value of a cell CLOSED at (pop) time te, else +inf
+    double closed_val(int64_t i, int64_t j, double te) const {
+      if (!in_grid(i, j)) return kInf;
+      const double t = pl.T((uint64_t)j * NX + i);
+      return (t <= t_closed && t <= te) ? t : kInf;
+    }
+    // the reference update (:504-535), -ffp-contract=off
+    static double eikonal(double tx, double ty, double C) {
+      if ((std::fabs(tx - ty) < C) && (tx < kInf) && (ty < kInf))
+        return (tx + ty + std::sqrt(2 * (C * C) - (tx - ty) * (tx - ty))) / 2;
+      return std::fmin(tx, ty) + C;
+    }
+    double axis(int64_t ia, int64_t ja, int64_t ib, int64_t jb, double te, int depth) {
+      const double a = closed_val(ia, ja, te), b = closed_val(ib, jb, te);
+      if (a < kInf || b < kInf) return std::fmin(a, b);  // OPEN sides are >= te >= it
+      const double va = in_grid(ia, ja) ? val((uint64_t)ja * NX + ia, te, depth + 1) : kInf;
+      const double vb = in_grid(ib, jb) ? val((uint64_t)jb * NX + ib, te, depth + 1) : kInf;
+      return std::fmin(va, vb);
+    }
+    double val(uint64_t k, double t, int depth) {
+      const double C = F[k];
+      if (!(C < kInf)) return kInf;       // obstacles are never updated
+      if (depth > 20000) return pl.T(k);  // pathological chains: the converged value
+      const auto key = std::make_pair(k, t);
+      auto it = memo.find(key);
+      if (it != memo.end()) return it->second;
+      const int64_t i = (int64_t)(k % NX), j = (int64_t)(k / NX);
+      double v = kInf;
+      const int64_t nb[4][2] = {{i, j - 1}, {i - 1, j}, {i + 1, j}, {i, j + 1}};
+      for (const auto& e : nb) {
+        const double te = closed_val(e[0], e[1], t);
+        if (!(te < kInf)) continue;  // not CLOSED by time t: no pop of it updated x yet
+        const double tx = axis(i - 1, j, i + 1, j, te, depth);
+        const double ty = axis(i, j - 1, i, j + 1, te, depth);
+        v = std::fmin(v, eikonal(tx, ty, C));
+      }
+      memo.emplace(key, v);
+      return v;
+    }
+  } rec{*this, speed_.data(), t_closed, (int64_t)nx_, (int64_t)ny_, {}};
+  out.resize(band.size());
+  for (size_t q = 0; q < band.size(); ++q) out[q] = rec.val(band[q], t_closed, 0);
 }
 
 // :443-468
@@ -298,7 +599,7 @@ bool DyMuPathPlanner::computeEntireTotalCostMap() {
     log_warn("The goal is not valid");
     return false;
   }
-  return solveFull();
+  return propagate(false, 0, 0);
 }
 
 // :410-422 (start and its 8 neighbours must be free; border -> false here,
@@ -311,12 +612,10 @@ bool DyMuPathPlanner::isSafeNode(unsigned i, unsigned j) const {
   return true;
 }
 
-// :364-408.  The reference stops its FMM once the start node and its nb4 are
-// CLOSED and returns false if the band is empty at that moment (start
-// unreachable, or the start's neighbourhood closes last of all).  The engine
-// converges the whole map; the return value is recovered from it: false iff
-// the start is unreachable or max T over {start, nb4} is the global maximum
-// finite T (those nodes close last).
+// :364-408.  The propagation stops once the start node and its nb4 are final
+// (dymu_solve_until_device); the return value is the reference's: false iff
+// the narrow band is empty at that moment (the start is unreachable, or its
+// neighbourhood closed last of all the reachable nodes).
 bool DyMuPathPlanner::computeTotalCostMap(base::Waypoint wPos) {
   const double x = wPos.position[0] - global_offset_[0];
   const double y = wPos.position[1] - global_offset_[1];
@@ -334,18 +633,7 @@ bool DyMuPathPlanner::computeTotalCostMap(base::Waypoint wPos) {
     log_error("PLANNER: The rover is located too close to an obstacle");
     return false;
   }
-  solveFull();
-  const uint64_t s = idx(si, sj);
-  if (!(total_cost_[s] < kInf)) {
-    log_error("The goal is unreachable");
-    return false;
-  }
-  double m = total_cost_[s];
-  for (uint64_t nb : {s - nx_, s - 1, s + 1, s + nx_}) m = std::max(m, total_cost_[nb]);
-  double tmax = 0;
-  for (double t : total_cost_)
-    if (t < kInf && t > tmax) tmax = t;
-  if (m >= tmax) {
+  if (!propagate(true, si, sj)) {
     log_error("The goal is unreachable");
     return false;
   }
@@ -432,9 +720,9 @@ base::Waypoint DyMuPathPlanner::computeNextGlobalWaypoint(base::Waypoint& wPos, 
 void DyMuPathPlanner::gradientNode(unsigned i, unsigned j, double& dnx, double& dny) const {
   const uint64_t k = idx(i, j);
   const bool hw = i > 0, he = i + 1 < nx_, hs = j > 0, hn = j + 1 < ny_;
-  const double tw = hw ? total_cost_[k - 1] : kInf, te = he ? total_cost_[k + 1] : kInf;
-  const double ts = hs ? total_cost_[k - nx_] : kInf, tn = hn ? total_cost_[k + nx_] : kInf;
-  const double t = total_cost_[k];
+  const double tw = hw ? T(k - 1) : kInf, te = he ? T(k + 1) : kInf;
+  const double ts = hs ? T(k - nx_) : kInf, tn = hn ? T(k + nx_) : kInf;
+  const double t = T(k);
   double dx, dy;
   if ((!hw && !he) || (hw && he && tw == kInf && te == kInf)) dx = 0;
   else if (!hw || tw == kInf) dx = te - t;
@@ -472,6 +760,7 @@ std::string DyMuPathPlanner::getLocomotionMode(base::Waypoint wPos) {
 
 // :799-811
 std::vector<std::vector<double>> DyMuPathPlanner::getTotalCostMatrix() {
+  fetchAll();
   std::vector<std::vector<double>> m(ny_, std::vector<double>(nx_));
   for (unsigned j = 0; j < ny_; ++j)
     for (unsigned i = 0; i < nx_; ++i) {
@@ -517,16 +806,16 @@ double DyMuPathPlanner::getTotalCost(base::Waypoint wInt) {
   if (i + 1 >= nx_ || j + 1 >= ny_) {  // a corner is NULL
     const unsigned ni = (unsigned)(x / global_res_ + 0.5), nj = (unsigned)(y / global_res_ + 0.5);
     if (ni >= nx_ || nj >= ny_) return kInf;
-    return total_cost_[idx(ni, nj)];
+    return T(idx(ni, nj));
   }
   const uint64_t k = idx(i, j);
   const uint64_t k10 = k + 1, k01 = k + nx_, k11 = k + nx_ + 1;
-  if (state_[k] == OPEN || state_[k10] == OPEN || state_[k01] == OPEN || state_[k11] == OPEN) {
+  if (!closedCell(k) || !closedCell(k10) || !closedCell(k01) || !closedCell(k11)) {
     const unsigned ni = (unsigned)(x / global_res_ + 0.5), nj = (unsigned)(y / global_res_ + 0.5);
-    return total_cost_[idx(ni, nj)];
+    return T(idx(ni, nj));
   }
-  const double w00 = total_cost_[k], w10 = total_cost_[k10];
-  const double w01 = total_cost_[k01], w11 = total_cost_[k11];
+  const double w00 = T(k), w10 = T(k10);
+  const double w01 = T(k01), w11 = T(k11);
   return w00 + (w10 - w00) * a + (w01 - w00) * b + (w11 + w00 - w10 - w01) * a * b;
 }
 

@@ -99,7 +99,85 @@ __global__ void k_theta_state(const unsigned long long* theta_bits, unsigned lon
   }
 }
 
+// ---- early exit of computeTotalCostMap (reference :364-408) ----
+
+__global__ void k_probe(const double* T, int64_t ld, ProbeCells cells,
+                        const unsigned long long* minkey, unsigned long long* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  unsigned long long m = 0;
+  for (int k = 0; k < cells.n; ++k) {
+    const unsigned long long b = dbits(T[cells.ij[k][1] * ld + cells.ij[k][0]]);
+    m = b > m ? b : m;  // T >= 0: bit order = value order
+  }
+  out[0] = m;
+  out[1] = minkey ? *minkey : kInfBits;
+}
+
+// Cells are CLOSED iff T <= t_closed (their values are final).  A cell that is not
+// CLOSED keeps its value only if it is in the band (a finite-speed 4-neighbour of a
+// CLOSED cell: the reference propagated into it, :462-465); every other cell was
+// never reached and gets +inf.  Writes only touch non-CLOSED cells and the test
+// reads only CLOSED-ness, so the races between threads do not change any answer.
+__global__ void k_early_mask(const double* F, double* T, int64_t ld, uint32_t nx, uint32_t ny,
+                             double tc, uint64_t* band, unsigned long long* n_band, uint64_t cap) {
+  const uint64_t n = (uint64_t)nx * ny;
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t j = (uint32_t)(c / nx), i = (uint32_t)(c % nx);
+    const int64_t k = (int64_t)j * ld + i;
+    const double t = T[k];
+    if (t <= tc) continue;  // CLOSED
+    bool b = false;
+    if (F[k] < __builtin_inf()) {
+      b = (j > 0 && T[k - ld] <= tc) || (i > 0 && T[k - 1] <= tc) ||
+          (i + 1 < nx && T[k + 1] <= tc) || (j + 1 < ny && T[k + ld] <= tc);
+    }
+    if (b) {
+      const unsigned long long pos = atomicAdd(n_band, 1ull);
+      if (pos < cap) band[pos] = c;
+    } else if (t < __builtin_inf()) {
+      T[k] = __builtin_inf();
+    }
+  }
+}
+
+__global__ void k_scatter(double* T, int64_t ld, uint32_t nx, const uint64_t* idx,
+                          const double* vals, uint64_t n) {
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t q = idx[c];
+    T[(int64_t)(q / nx) * ld + (int64_t)(q % nx)] = vals[c];
+  }
+}
+
 }  // namespace
+
+hipError_t launch_probe(const double* T, int64_t ld, const ProbeCells& cells,
+                        const unsigned long long* minkey, unsigned long long* out,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, st, T, ld, cells, minkey, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_early_mask(const double* F, double* T, int64_t ld, uint32_t nx, uint32_t ny,
+                             double t_closed, uint64_t* band, unsigned long long* n_band,
+                             uint64_t cap, hipStream_t st) {
+  uint64_t b = ((uint64_t)nx * ny + 255) / 256;
+  if (b > 16384) b = 16384;
+  if (b == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_early_mask, dim3((unsigned)b), dim3(256), 0, st, F, T, ld, nx, ny,
+                     t_closed, band, n_band, cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter(double* T, int64_t ld, uint32_t nx, const uint64_t* idx,
+                          const double* vals, uint64_t n, hipStream_t st) {
+  uint64_t b = (n + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scatter, dim3((unsigned)b), dim3(256), 0, st, T, ld, nx, idx, vals, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_window_min(const double* T, int64_t ld, uint32_t i0, uint32_t j0, uint32_t i1,
                              uint32_t j1, unsigned long long* out, hipStream_t st) {

@@ -129,6 +129,18 @@ FIM_SYMBOLS = {
                                           _u32, _u32, _u32, _vp, ctypes.POINTER(DymuStats)]),
     "dymu_resolve_window": (_i32, [_vp, _dp, _u32, _u32, _u32, _u32, _u32, _u32, _u32, _u32,
                                    _dp, ctypes.POINTER(DymuStats)]),
+    "dymu_solve_until_device": (_i32, [_vp, _vp, _vp, _u32, _u32, _u64, _u32, _u32, _u32, _u32,
+                                       _vp, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(DymuStats)]),
+    "dymu_early_exit_mask": (_i32, [_vp, _vp, _vp, _u32, _u32, _u64, ctypes.c_double, _vp, _u64,
+                                    ctypes.POINTER(_u64), _vp]),
+    "dymu_scatter": (_i32, [_vp, _vp, _u32, _u64, _vp, _vp, _u64, _vp]),
+    "dymu_memcpy2d_d2h": (_i32, [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t,
+                                 ctypes.c_size_t, ctypes.c_size_t]),
+    "dymu_memcpy2d_h2d": (_i32, [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t,
+                                 ctypes.c_size_t, ctypes.c_size_t]),
+    "dymu_host_register": (_i32, [_vp, _vp, ctypes.c_size_t]),
+    "dymu_host_unregister": (_i32, [_vp, _vp]),
     "dymu_get_stream": (_vp, [_vp]),
     "dymu_strerror": (ctypes.c_char_p, [_i32]),
     "dymu_last_error": (ctypes.c_char_p, [_vp]),
@@ -247,6 +259,17 @@ class Engine:
         _check(self._lib.dymu_solve_device(self.ctx, dF, dT, nx, ny, ld, goal_i, goal_j,
                                            stream or None, ctypes.byref(st)), self.ctx)
         return st.as_dict()
+
+    def solve_until_device(self, dF: int, dT: int, nx: int, ny: int, ld: int, goal_i: int,
+                           goal_j: int, start_i: int, start_j: int, stream: int = 0):
+        """computeTotalCostMap's propagation: stops once the start and its nb4 are final.
+        Returns (t_closed, stats)."""
+        st = DymuStats()
+        tc = ctypes.c_double()
+        _check(self._lib.dymu_solve_until_device(self.ctx, dF, dT, nx, ny, ld, goal_i, goal_j,
+                                                 start_i, start_j, stream or None,
+                                                 ctypes.byref(tc), ctypes.byref(st)), self.ctx)
+        return tc.value, st.as_dict()
 
     def synth_speed(self, dF: int, nx: int, ny: int, ld: int, row0: int = 0, seed: int = 1,
                     obst_frac: float = 0.0, obst_seed: int = 3, goal_i: int = 0,

@@ -66,6 +66,23 @@ def main():
     out["early64_T"] = T
     out["early64_closed"] = closed
     out["early64_rc"] = np.array([rc], dtype=np.int64)
+    # 4) early exit far from the goal on a 256^2 map: U(1,5) from
+    #    mt19937_64(5), 3% obstacles, goal (200, 190), start (30, 40)
+    N = 256
+    cost = o.mt_uniform(N * N, seed=5).reshape(N, N)
+    obs_u = o.mt_uniform(N * N, seed=6, lo=0.0, hi=1.0).reshape(N, N)
+    cost[obs_u < 0.03] = -1.0
+    g, s = (200, 190), (30, 40)
+    for (ci, cj) in (g, s):
+        cost[cj - 1:cj + 2, ci - 1:ci + 2] = np.abs(cost[cj - 1:cj + 2, ci - 1:ci + 2])
+    F = o.pack_speed(*(lambda t: (t["cost"], t["hazard"], t["traff"], t["is_obstacle"]))(
+        _state_from_cost(o, cost)), res=1.0)
+    T, rc, closed = o.fmm(F, g, start=s, linear=False, want_closed=True)
+    out["early256_cost"] = cost
+    out["early256_goal_start"] = np.array(g + s, dtype=np.int64)
+    out["early256_T"] = T
+    out["early256_closed"] = closed
+    out["early256_rc"] = np.array([rc], dtype=np.int64)
     for k, v in out.items():
         np.save(os.path.join(HERE, k + ".npy"), v, allow_pickle=False)
     print("wrote", len(out), "fixtures")

@@ -142,8 +142,9 @@ def test_auto_kernel_choice(dymu):
         assert r.T[3, 13] == 10.0  # on the axis through the goal: the distance
     finally:
         eng.close()
-    with pytest.raises(dymu.DymuError):
-        dymu.Engine(kernel=7)
+    for k in (1, 2, 6, 7, -1):  # only 0 (auto) and 3-5 exist (kernels 1/2 were removed)
+        with pytest.raises(dymu.DymuError):
+            dymu.Engine(kernel=k)
 
 
 def test_bad_args(engine, dymu):

@@ -103,8 +103,21 @@ def test_entire_total_cost_map_terrain(dymu, oracle):
     assert (np.abs(T[fin] - Tref[fin]) / np.maximum(1, Tref[fin])).max() <= RTOL
 
 
+def _early_matches(M, Tt):
+    """getTotalCostMatrix after computeTotalCostMap vs the reference's early-exit
+    state: the never-reached mask (-1) exact, CLOSED values and the band's
+    tentative values within the parity tolerance."""
+    ref = np.where(np.isinf(Tt), -1.0, Tt)
+    assert np.array_equal(M == -1.0, ref == -1.0)
+    fin = ref >= 0
+    assert (np.abs(M[fin] - ref[fin]) / np.maximum(1, ref[fin])).max() <= RTOL
+
+
 @pytest.mark.gpu
 def test_compute_total_cost_map_returns(dymu, oracle):
+    """computeTotalCostMap (:364-408) stops like the reference: the whole
+    getTotalCostMatrix -- CLOSED values, the band's tentative values and -1 for
+    the cells never reached -- equals the reference's early-exit state."""
     cost = gold("setcost64_cost")
     g = tuple(int(x) for x in gold("setcost64_goal"))
     N = cost.shape[0]
@@ -112,15 +125,102 @@ def test_compute_total_cost_map_returns(dymu, oracle):
     p.initGlobalLayer(1.0, 0.5, N, N)
     p.setCostMap(cost)
     p.setGoal(g)
-    # the golden early-exit run: reference returns 1 and has closed the start
     assert p.computeTotalCostMap((12, 50)) == bool(gold("early64_rc")[0])
-    T = p.totalCostRaw()
-    Tt, closed = gold("early64_T"), gold("early64_closed").astype(bool)
-    # CLOSED cells hold final values in the reference; they must agree
-    assert (np.abs(T[closed] - Tt[closed]) / np.maximum(1, Tt[closed])).max() <= RTOL
+    _early_matches(p.getTotalCostMatrix(), gold("early64_T"))
+    assert p.lastBandSize() > 0
     assert not p.computeTotalCostMap((0.2, 30))        # border start: unsafe
     obs = np.argwhere(cost <= 0)[0]
     assert not p.computeTotalCostMap((obs[1], obs[0]))  # on an obstacle
+
+
+@pytest.mark.gpu
+def test_early_exit_far_start_256(dymu, oracle):
+    """A start far from the goal on a 256^2 map with obstacles (golden from the
+    oracle's exact reference pop order)."""
+    cost = gold("early256_cost")
+    gi, gj, si, sj = (int(x) for x in gold("early256_goal_start"))
+    N = cost.shape[0]
+    p = dymu.Planner()
+    p.initGlobalLayer(1.0, 0.5, N, N)
+    p.setCostMap(cost)
+    assert p.setGoal((gi, gj))
+    assert p.computeTotalCostMap((si, sj)) == bool(gold("early256_rc")[0])
+    _early_matches(p.getTotalCostMatrix(), gold("early256_T"))
+    # the state drives getTotalCost's CLOSED test (:873-876) like the reference's
+    closed = gold("early256_closed").astype(bool)
+    Tt = gold("early256_T")
+    for (x, y) in [(si + 0.3, sj + 0.6), (gi - 2.5, gj + 0.25), (100.5, 100.5)]:
+        i, j = int(x), int(y)
+        a, b = x - i, y - j
+        if closed[j, i] and closed[j, i + 1] and closed[j + 1, i] and closed[j + 1, i + 1]:
+            w00, w10, w01, w11 = Tt[j, i], Tt[j, i + 1], Tt[j + 1, i], Tt[j + 1, i + 1]
+            exp = w00 + (w10 - w00) * a + (w01 - w00) * b + (w11 + w00 - w10 - w01) * a * b
+        else:
+            exp = Tt[int(y + 0.5), int(x + 0.5)]
+        got = p.getTotalCost((x, y))
+        assert (np.isinf(exp) and np.isinf(got)) or abs(got - exp) <= RTOL * max(1, abs(exp))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(6))
+def test_early_exit_random_vs_oracle(dymu, oracle, seed):
+    """Random maps and starts against the oracle's early exit; a start next to
+    the goal runs fewer passes than the full solve."""
+    rng = np.random.default_rng(100 + seed)
+    N = int(rng.integers(48, 160))
+    g = (int(rng.integers(4, N - 4)), int(rng.integers(4, N - 4)))
+    F = oracle.synth_speed(N, N, seed=200 + seed, obst_frac=0.04, obst_seed=300 + seed, goal=g)
+    cost = np.where(np.isfinite(F), F, -1.0)
+    for _ in range(200):
+        s = (int(rng.integers(2, N - 2)), int(rng.integers(2, N - 2)))
+        if np.isfinite(F[s[1] - 1:s[1] + 2, s[0] - 1:s[0] + 2]).all():
+            break
+    assert np.isfinite(F[s[1] - 1:s[1] + 2, s[0] - 1:s[0] + 2]).all()
+    p = dymu.Planner()
+    p.initGlobalLayer(1.0, 0.5, N, N)
+    p.setCostMap(cost)
+    assert p.setGoal(g)
+    Tt, rc, _ = oracle.fmm(F, g, start=s, want_closed=True)
+    assert p.computeTotalCostMap(s) == bool(rc)
+    _early_matches(p.getTotalCostMatrix(), Tt)
+    # near start: fewer passes than computeEntireTotalCostMap
+    near = (g[0] + 1, g[1])
+    p.computeTotalCostMap(near)
+    near_passes = p.lastStats()["passes"]
+    p.computeEntireTotalCostMap()
+    assert near_passes < p.lastStats()["passes"]
+
+
+@pytest.mark.gpu
+def test_early_exit_false_returns(dymu, oracle):
+    """The reference returns false when the band is empty at exit (:399-403):
+    a start enclosed by obstacles (unreachable), and a start whose neighbourhood
+    closes last of all the reachable nodes (expensive start cells)."""
+    N = 40
+    cost = np.ones((N, N))
+    cost[24:33, 24:33] = -1.0
+    cost[25:32, 25:32] = 1.0   # a free room inside a wall: unreachable
+    p = dymu.Planner()
+    p.initGlobalLayer(1.0, 0.5, N, N)
+    p.setCostMap(cost)
+    assert p.setGoal((8, 8))
+    F = np.where(cost > 0, cost * 1.0, np.inf)
+    Tt, rc, _ = oracle.fmm(F, (8, 8), start=(28, 28), want_closed=True)
+    assert rc == 0
+    assert not p.computeTotalCostMap((28, 28))
+    _early_matches(p.getTotalCostMatrix(), Tt)
+    cost2 = np.ones((N, N))
+    for (i, j) in [(20, 20), (20, 19), (19, 20), (21, 20), (20, 21)]:
+        cost2[j, i] = 1000.0  # the start and its nb4 close after everything else
+    p2 = dymu.Planner()  # setCostMap never clears an obstacle flag (:117-123)
+    p2.initGlobalLayer(1.0, 0.5, N, N)
+    p2.setCostMap(cost2)
+    assert p2.setGoal((8, 8))
+    F2 = cost2 * 1.0
+    Tt2, rc2, _ = oracle.fmm(F2, (8, 8), start=(20, 20), want_closed=True)
+    assert rc2 == 0
+    assert not p2.computeTotalCostMap((20, 20))
+    _early_matches(p2.getTotalCostMatrix(), Tt2)
 
 
 @pytest.mark.gpu
