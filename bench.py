@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--size", type=int, default=16384)
     ap.add_argument("--obst", type=float, default=0.02)
-    ap.add_argument("--cpu-sample", type=int, default=8192,
+    ap.add_argument("--cpu-sample", type=int, default=16384,
                     help="edge of the grid the CPU baseline solves (0 = skip)")
     ap.add_argument("--no-profile", action="store_true",
                     help="no per-launch events (roofline reported as null)")
@@ -64,6 +64,9 @@ def parse():
                          "python loop; tools/vdist_rehearsal.py)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the row-slab path even at N=1 (exercises the RCCL code path)")
+    ap.add_argument("--no-planner", action="store_true",
+                    help="skip the class-surface leg (computeEntireTotalCostMap through "
+                         "libdymu_planner.so)")
     ap.add_argument("--fake-cpu", action="store_true",
                     help="tests only: the N-rank plumbing on CPU (gloo, numpy stand-in engine, "
                          "python exchange loop); no GPU is touched")
@@ -87,6 +90,20 @@ def spawn_ranks(n):
     return subprocess.call(cmd)
 
 
+def host_cpu():
+    """The host the CPU baseline ran on: logical CPUs and the model name."""
+    model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "model": model}
+
+
 def cpu_baseline(n_edge, obst):
     """Oracle heap FMM (reference pop order) on an n_edge^2 config-3 grid, 1 thread."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -104,8 +121,8 @@ def cpu_baseline(n_edge, obst):
         "cores": 1,
         "kind": "port",
         "sample": f"{n_edge}x{n_edge} config-3 grid (2% obstacles, goal centre), oracle heap "
-                  f"FMM with the reference's pop order, 1 thread, {dt:.1f}s; "
-                  f"host {platform.processor() or platform.machine()}",
+                  f"FMM with the reference's pop order, 1 thread, {dt:.1f}s",
+        "host": host_cpu(),
     }
 
 
@@ -174,6 +191,51 @@ def run_single(args):
     eng.free(dT)
     eng.close()
     return dt, tot, kern_ms, kern_n, st
+
+
+def planner_leg(N, obst, steps):
+    """The drop-in class surface at the headline size: computeEntireTotalCostMap
+    (reference :443-468) through libdymu_planner.so (include/DyMu.hpp), the call a
+    Rock caller makes.  Each step moves the goal between two valid cells, so every
+    step is a cold solve (no map reuse); the speed stays resident on the device and
+    the total cost is not downloaded.  Returns ms per step and the same for a step
+    that also reads the whole map back (getTotalCostMatrix's download)."""
+    import dymu
+
+    g = (N // 2, N // 2)
+    eng = dymu.Engine(device=int(os.environ.get("LOCAL_RANK", "0")))
+    dF = eng.alloc(8 * N * N)
+    eng.synth_speed(dF, N, N, N, 0, 1, obst, 3, g[0], g[1])
+    F = np.empty((N, N))
+    eng.d2h(F, dF)
+    eng.free(dF)
+    eng.close()
+    cost = np.where(np.isfinite(F), F, -1.0)
+    del F
+    p = dymu.Planner(device=int(os.environ.get("LOCAL_RANK", "0")))
+    p.initGlobalLayer(1.0, 0.5, N, N)
+    p.setCostMap(cost)
+    goals = [g]
+    for d in range(1, 64):  # a second valid goal next to the first
+        if p.setGoal((g[0] + d, g[1])):
+            goals.append((g[0] + d, g[1]))
+            break
+    del cost
+    p.setGoal(goals[0])
+    p.computeEntireTotalCostMap()  # uploads the speed once
+    t0 = time.perf_counter()
+    for k in range(steps):
+        p.setGoal(goals[(k + 1) % len(goals)])
+        p.computeEntireTotalCostMap()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    t0 = time.perf_counter()
+    p.setGoal(goals[0])
+    p.computeEntireTotalCostMap()
+    p.totalCostRaw()
+    ms_read = (time.perf_counter() - t0) * 1e3
+    kind = p.lastSolveKind()
+    p.close()
+    return ms, ms_read, kind
 
 
 def main():
@@ -301,6 +363,17 @@ def main():
     }
     if args.fake_cpu:
         line["data"] = "synthetic; --fake-cpu plumbing rehearsal (numpy engine, not a GPU number)"
+    if world == 1 and not args.no_planner and not args.fake_cpu and not args.sharded:
+        pms, pms_read, kind = planner_leg(N, args.obst, max(2, min(K, 5)))
+        line["planner"] = {
+            "api": "DyMuPathPlanner::computeEntireTotalCostMap via libdymu_planner.so (C-ABI)",
+            "ms_per_step": round(pms, 3),
+            "ratio_to_engine": round(pms / (dt / K * 1e3), 3),
+            "ms_with_full_map_readback": round(pms_read, 3),
+            "note": "goal alternates between two cells, so every step is a cold solve; the "
+                    "readback step adds getTotalCostMatrix's 2 GiB D2H",
+            "last_solve_kind": kind,
+        }
     if world == 1 and args.cpu_sample > 0 and not args.fake_cpu:
         line["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.obst)
         line["cpu_reference_algorithm"] = cpu_reference_algorithm(1024, args.obst)

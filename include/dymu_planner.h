@@ -66,6 +66,14 @@ int dymu_planner_get_locomotion_mode(dymu_planner* p, double x, double y, double
 /* dynamic feedback (extension): hazard_density / trafficability, ny*nx */
 int dymu_planner_set_hazard_density(dymu_planner* p, const double* hd);
 int dymu_planner_set_trafficability(dymu_planner* p, const double* tr);
+/* windowed forms: w*h values (row-major) for cells [i0, i0+w) x [j0, j0+h) */
+int dymu_planner_set_hazard_density_window(dymu_planner* p, uint32_t i0, uint32_t j0, uint32_t w,
+                                           uint32_t h, const double* hd);
+int dymu_planner_set_trafficability_window(dymu_planner* p, uint32_t i0, uint32_t j0, uint32_t w,
+                                           uint32_t h, const double* tr);
+/* narrow-band cells left by the last computeTotalCostMap's early exit (0 after
+ * computeEntireTotalCostMap) */
+int64_t dymu_planner_last_band_size(dymu_planner* p);
 /* statistics of the last solve */
 int dymu_planner_last_stats(dymu_planner* p, dymu_stats* out);
 /* how the last solve ran: 0 cold, 1 windowed re-propagation from the window

@@ -208,4 +208,21 @@ int dymu_planner_last_solve_kind(dymu_planner* p) {
   return p->pl.lastSolveKind();
 }
 
+int dymu_planner_set_hazard_density_window(dymu_planner* p, uint32_t i0, uint32_t j0, uint32_t w,
+                                           uint32_t h, const double* hd) {
+  if (!p || !hd) return DYMU_ERR_ARG;
+  return guarded([&] { return (int)p->pl.setHazardDensityWindow(i0, j0, w, h, hd); });
+}
+
+int dymu_planner_set_trafficability_window(dymu_planner* p, uint32_t i0, uint32_t j0, uint32_t w,
+                                           uint32_t h, const double* tr) {
+  if (!p || !tr) return DYMU_ERR_ARG;
+  return guarded([&] { return (int)p->pl.setTrafficabilityWindow(i0, j0, w, h, tr); });
+}
+
+int64_t dymu_planner_last_band_size(dymu_planner* p) {
+  if (!p) return DYMU_ERR_ARG;
+  return (int64_t)p->pl.lastBandSize();
+}
+
 }  // extern "C"

@@ -409,6 +409,9 @@ PLANNER_SYMBOLS = {
     "dymu_planner_set_trafficability": (_i32, [_vp, _dp]),
     "dymu_planner_last_stats": (_i32, [_vp, ctypes.POINTER(DymuStats)]),
     "dymu_planner_last_solve_kind": (_i32, [_vp]),
+    "dymu_planner_set_hazard_density_window": (_i32, [_vp, _u32, _u32, _u32, _u32, _dp]),
+    "dymu_planner_set_trafficability_window": (_i32, [_vp, _u32, _u32, _u32, _u32, _dp]),
+    "dymu_planner_last_band_size": (ctypes.c_int64, [_vp]),
 }
 
 _pl = None
@@ -555,6 +558,20 @@ class Planner:
 
     def setTrafficability(self, tr) -> bool:
         return _b(self._lib.dymu_planner_set_trafficability(self.h, self._grid(tr)))
+
+    def setHazardDensityWindow(self, i0: int, j0: int, hd) -> bool:
+        a = np.ascontiguousarray(hd, dtype=np.float64)
+        h, w = a.shape
+        return _b(self._lib.dymu_planner_set_hazard_density_window(self.h, i0, j0, w, h, a))
+
+    def setTrafficabilityWindow(self, i0: int, j0: int, tr) -> bool:
+        a = np.ascontiguousarray(tr, dtype=np.float64)
+        h, w = a.shape
+        return _b(self._lib.dymu_planner_set_trafficability_window(self.h, i0, j0, w, h, a))
+
+    def lastBandSize(self) -> int:
+        """Narrow-band cells left by the last computeTotalCostMap (0 after a full solve)."""
+        return _b_int(self._lib.dymu_planner_last_band_size(self.h))
 
     def lastSolveKind(self) -> int:
         """0 cold solve, 1 windowed re-propagation, 2 previous map reused."""

@@ -27,6 +27,27 @@ def terrain_inputs(N):
     return elev, terr, lut, slopes
 
 
+def valuenoise(N, seed=2, cell=64):
+    """Bilinear value noise on a `cell`-spaced lattice of U(0,1) draws (SURVEY s8(d)
+    config 2's elevation term)."""
+    L = N // cell + 2
+    rng = np.random.default_rng(seed)
+    lat = rng.uniform(0.0, 1.0, (L, L))
+    x = np.arange(N) / cell
+    i0 = np.floor(x).astype(int)
+    f = x - i0
+    rows = lat[:, i0] * (1 - f) + lat[:, i0 + 1] * f          # [L, N] along x
+    return rows[i0, :] * (1 - f)[:, None] + rows[i0 + 1, :] * f[:, None]
+
+
+def config2_inputs(N):
+    """BASELINE config 2: elevation 3 sin(0.05 i) cos(0.07 j) + 0.002 i +
+    0.5 valuenoise(seed 2, 64-cell lattice); terrain 1 + ((i/16 + j/16) mod 2); LUT
+    3 terrains x "Wheel" x slopes {0,5,10,15,20} deg."""
+    elev, terr, lut, slopes = terrain_inputs(N)
+    return elev + 0.5 * valuenoise(N), terr, lut, slopes
+
+
 def main():
     o = oracle_ffi.load()
     out = {}

@@ -22,25 +22,7 @@ import numpy as np  # noqa: E402
 import dymu  # noqa: E402
 
 
-def valuenoise(N, seed=2, cell=64):
-    """Bilinear value noise on a `cell`-spaced lattice of U(0,1) draws."""
-    L = N // cell + 2
-    rng = np.random.default_rng(seed)
-    lat = rng.uniform(0.0, 1.0, (L, L))
-    x = np.arange(N) / cell
-    i0 = np.floor(x).astype(int)
-    f = x - i0
-    rows = lat[:, i0] * (1 - f) + lat[:, i0 + 1] * f          # [L, N] along x
-    return rows[i0, :] * (1 - f)[:, None] + rows[i0 + 1, :] * f[:, None]
-
-
-def config2_inputs(N):
-    j, i = np.mgrid[0:N, 0:N].astype(np.float64)
-    elev = 3.0 * np.sin(0.05 * i) * np.cos(0.07 * j) + 0.002 * i + 0.5 * valuenoise(N)
-    terr = 1.0 + (((i.astype(np.int64) // 16) + (j.astype(np.int64) // 16)) % 2)
-    lut = np.array([100.0] * 5 + [1, 1.5, 2, 3, 5] + [2, 2.5, 3, 4, 6], dtype=np.float64)
-    slopes = np.array([0.0, 5.0, 10.0, 15.0, 20.0])
-    return elev, terr, lut, slopes
+from gen_golden import config2_inputs  # noqa: E402  (SURVEY s8(d) config 2 inputs)
 
 
 FIELDS = {"cost": 8, "raw_cost": 8, "slope": 8, "terrain": 4, "is_obstacle": 1, "hazard": 8,
