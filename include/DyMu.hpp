@@ -172,6 +172,7 @@ class DyMuPathPlanner {
   std::vector<double> speed_;
   std::vector<double> row_;
   bool speed_valid_ = false;
+  bool decrease_only_ = false;  // the last syncSpeed changed no speed upwards
   unsigned dirty_j0_ = 0, dirty_j1_ = 0;
   bool solved_ = false;  // dT_ holds the converged map of speed_ for the goal below
   unsigned solved_gi_ = 0, solved_gj_ = 0;

@@ -218,6 +218,16 @@ int dymu_resolve_window_device(dymu_ctx* ctx, const double* dF, double* dT, uint
                                uint32_t ny, uint64_t ld, uint32_t goal_i, uint32_t goal_j,
                                uint32_t i0, uint32_t j0, uint32_t w, uint32_t h, void* stream,
                                dymu_stats* stats);
+/* The same with the caller's knowledge of the change: decrease_only != 0
+ * promises that no speed in the window increased (a trafficability drop,
+ * reference src/DyMu_LocalPathRepairing.cpp:389-394, or a cleared hazard).  Then
+ * the old map is a valid upper bound everywhere and no cell is reset: only the
+ * window's tiles are seeded and the passes lower what the cheaper window
+ * reaches.  decrease_only = 0 is dymu_resolve_window_device. */
+int dymu_update_window_device(dymu_ctx* ctx, const double* dF, double* dT, uint32_t nx,
+                              uint32_t ny, uint64_t ld, uint32_t goal_i, uint32_t goal_j,
+                              uint32_t i0, uint32_t j0, uint32_t w, uint32_t h, int decrease_only,
+                              void* stream, dymu_stats* stats);
 /* Host-buffer form: requires that the previous dymu_solve / dymu_resolve_window
  * on this context solved the same grid size and goal (DYMU_ERR_STATE otherwise);
  * only the window of F is uploaded, the whole new T is written to T_out. */

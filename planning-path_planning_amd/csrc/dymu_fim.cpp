@@ -562,9 +562,11 @@ int solve_until_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uin
 
 // Windowed re-propagation (update_kernels.hip): dT holds the converged map of
 // the previous speed, dF the new speed, which differs only inside the window.
+// decrease_only: the caller guarantees no speed in the window went up; then the
+// old map is kept whole and only the window's tiles are seeded (k_seed_window).
 int resolve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
                  uint32_t gi, uint32_t gj, uint32_t i0, uint32_t j0, uint32_t w, uint32_t h,
-                 hipStream_t st, dymu_stats* stats) {
+                 hipStream_t st, dymu_stats* stats, bool decrease_only = false) {
   if (gi >= nx || gj >= ny || w == 0 || h == 0 || i0 >= nx || j0 >= ny) return DYMU_ERR_ARG;
   int rc = dom_begin(c, dF, dT, nx, ny, ld, 0, 0, -1, -1, st, /*cold=*/false);
   if (rc) return rc;
@@ -599,7 +601,10 @@ int resolve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_
     u.hist = prio_hist(c, 0);
     HIPC(c, launch_theta_state(theta, prio_minkey(c, 0), prio_base(c, 0), st));
   }
-  HIPC(c, launch_reset_seed(u, st));
+  if (decrease_only)
+    HIPC(c, launch_seed_window(u, i0, j0, i0 + w, j0 + h, st));
+  else
+    HIPC(c, launch_reset_seed(u, st));
   return converge(c, st, stats);
 }
 
@@ -858,6 +863,18 @@ int dymu_resolve_window_device(dymu_ctx* c, const double* dF, double* dT, uint32
   w = (uint32_t)std::min<uint64_t>(w, nx > i0 ? nx - i0 : 0);
   h = (uint32_t)std::min<uint64_t>(h, ny > j0 ? ny - j0 : 0);
   return resolve_core(c, dF, dT, nx, ny, ld, gi, gj, i0, j0, w, h, pick_stream(c, stream), stats);
+}
+
+int dymu_update_window_device(dymu_ctx* c, const double* dF, double* dT, uint32_t nx,
+                              uint32_t ny, uint64_t ld, uint32_t gi, uint32_t gj, uint32_t i0,
+                              uint32_t j0, uint32_t w, uint32_t h, int decrease_only, void* stream,
+                              dymu_stats* stats) {
+  if (!c || !dF || !dT || nx == 0 || ny == 0 || ld < nx) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  w = (uint32_t)std::min<uint64_t>(w, nx > i0 ? nx - i0 : 0);
+  h = (uint32_t)std::min<uint64_t>(h, ny > j0 ? ny - j0 : 0);
+  return resolve_core(c, dF, dT, nx, ny, ld, gi, gj, i0, j0, w, h, pick_stream(c, stream), stats,
+                      decrease_only != 0);
 }
 
 int dymu_resolve_window(dymu_ctx* c, const double* F, uint32_t nx, uint32_t ny, uint32_t gi,

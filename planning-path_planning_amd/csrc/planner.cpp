@@ -364,6 +364,7 @@ bool DyMuPathPlanner::syncSpeed(unsigned& i0, unsigned& i1, unsigned& j0, unsign
   i1 = 0;
   j0 = ny_;
   j1 = 0;
+  decrease_only_ = speed_valid_;
   if (dirty_j0_ >= dirty_j1_ && speed_valid_) return false;
   const unsigned d0 = speed_valid_ ? dirty_j0_ : 0, d1 = speed_valid_ ? dirty_j1_ : ny_;
   row_.resize(nx_);
@@ -379,6 +380,8 @@ bool DyMuPathPlanner::syncSpeed(unsigned& i0, unsigned& i1, unsigned& j0, unsign
     if (speed_valid_) {
       while (std::memcmp(&row_[a], old + a, sizeof(double)) == 0) ++a;
       while (std::memcmp(&row_[b - 1], old + b - 1, sizeof(double)) == 0) --b;
+      for (unsigned i = a; i < b && decrease_only_; ++i)
+        if (!(row_[i] <= old[i])) decrease_only_ = false;
     }
     std::memcpy(old, row_.data(), sizeof(double) * nx_);
     i0 = std::min(i0, a);
@@ -445,7 +448,8 @@ bool DyMuPathPlanner::closedCell(uint64_t k) const {
 // computeEntireTotalCostMap (:443-468), incremental where possible: when dT_
 // holds the converged map of the same grid and goal and the speed changed only
 // inside a window (the local layer's hazard / trafficability writes), the engine
-// re-propagates from that window (dymu_resolve_window_device); unchanged speed
+// re-propagates from that window (dymu_update_window_device; without any reset
+// when every changed speed went down); unchanged speed
 // reuses the map.  Both give the cold solve's fixed point.
 // Returns false iff the early exit left an empty band (the reference's "goal
 // unreachable" return, :399-403).
@@ -461,8 +465,8 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
       return true;
     }
     if ((uint64_t)(i1 - i0) * (j1 - j0) * 4 <= n) {
-      rc = dymu_resolve_window_device(ctx_, dF_, dT_, nx_, ny_, nx_, goal_i_, goal_j_, i0, j0,
-                                      i1 - i0, j1 - j0, nullptr, &stats_);
+      rc = dymu_update_window_device(ctx_, dF_, dT_, nx_, ny_, nx_, goal_i_, goal_j_, i0, j0,
+                                     i1 - i0, j1 - j0, decrease_only_ ? 1 : 0, nullptr, &stats_);
       if (rc == DYMU_OK) incremental_ = 1;
     }
   }

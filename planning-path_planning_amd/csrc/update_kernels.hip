@@ -89,6 +89,29 @@ __global__ void k_reset_seed(UpdateArgs a) {
   }
 }
 
+// Decrease-only change (every speed in W went down or stayed): the old map is a
+// valid upper bound of the new fixed point everywhere, and a cell whose value
+// changes has a new optimal path entering W from its ring, so its new value is
+// above min old T over the ring >= theta; no cell needs a reset.  Seed every tile
+// that intersects W (tiles [tx0,tx1) x [ty0,ty1)) with key theta; the passes
+// then lower whatever the cheaper window reaches.
+__global__ void k_seed_window(UpdateArgs a, uint32_t tx0, uint32_t ty0, uint32_t tx1,
+                              uint32_t ty1) {
+  const uint32_t w = tx1 - tx0, n = w * (ty1 - ty0);
+  const uint32_t shard = blockIdx.x % kShards;
+  for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
+    const uint32_t tile = (ty0 + c / w) * a.ntx + (tx0 + c % w);
+    if (atomicMax(&a.tile_epoch[tile], a.epoch) < a.epoch) {
+      const uint32_t pos = atomicAdd(&a.counts[shard], 1u);
+      a.list[(uint64_t)shard * a.shard_cap + pos] = tile;
+      if (a.keys) {
+        atomicMin(&a.keys[tile], *a.theta_bits);
+        atomicAdd(&a.hist[shard * kBins], 1u);
+      }
+    }
+  }
+}
+
 // Priority-kernel list-0 state: keys of the seeded tiles are theta.
 __global__ void k_theta_state(const unsigned long long* theta_bits, unsigned long long* minkey0,
                               double* base0) {
@@ -194,6 +217,18 @@ hipError_t launch_reset_seed(const UpdateArgs& a, hipStream_t st) {
   if (b > 8192) b = 8192;
   if (b == 0) b = 1;
   hipLaunchKernelGGL(k_reset_seed, dim3((unsigned)b), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_seed_window(const UpdateArgs& a, uint32_t i0, uint32_t j0, uint32_t i1,
+                              uint32_t j1, hipStream_t st) {
+  const uint32_t tx0 = i0 / a.tw, ty0 = j0 / a.th;
+  const uint32_t tx1 = (i1 + a.tw - 1) / a.tw, ty1 = (j1 + a.th - 1) / a.th;
+  const uint64_t n = (uint64_t)(tx1 - tx0) * (ty1 - ty0);
+  uint64_t b = (n + 255) / 256;
+  if (b > 1024) b = 1024;
+  if (b == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_seed_window, dim3((unsigned)b), dim3(256), 0, st, a, tx0, ty0, tx1, ty1);
   return hipGetLastError();
 }
 

@@ -127,6 +127,9 @@ FIM_SYMBOLS = {
                                ctypes.POINTER(DymuCostState), _vp, _vp]),
     "dymu_resolve_window_device": (_i32, [_vp, _vp, _vp, _u32, _u32, _u64, _u32, _u32, _u32,
                                           _u32, _u32, _u32, _vp, ctypes.POINTER(DymuStats)]),
+    "dymu_update_window_device": (_i32, [_vp, _vp, _vp, _u32, _u32, _u64, _u32, _u32, _u32,
+                                         _u32, _u32, _u32, _i32, _vp,
+                                         ctypes.POINTER(DymuStats)]),
     "dymu_resolve_window": (_i32, [_vp, _dp, _u32, _u32, _u32, _u32, _u32, _u32, _u32, _u32,
                                    _dp, ctypes.POINTER(DymuStats)]),
     "dymu_solve_until_device": (_i32, [_vp, _vp, _vp, _u32, _u32, _u64, _u32, _u32, _u32, _u32,
@@ -250,6 +253,15 @@ class Engine:
         _check(self._lib.dymu_resolve_window_device(self.ctx, dF, dT, nx, ny, ld, goal_i, goal_j,
                                                     i0, j0, w, h, stream or None,
                                                     ctypes.byref(st)), self.ctx)
+        return st.as_dict()
+
+    def update_window_device(self, dF: int, dT: int, nx: int, ny: int, ld: int, goal_i: int,
+                             goal_j: int, i0: int, j0: int, w: int, h: int,
+                             decrease_only: bool, stream: int = 0) -> dict:
+        st = DymuStats()
+        _check(self._lib.dymu_update_window_device(self.ctx, dF, dT, nx, ny, ld, goal_i, goal_j,
+                                                   i0, j0, w, h, int(bool(decrease_only)),
+                                                   stream or None, ctypes.byref(st)), self.ctx)
         return st.as_dict()
 
     # -- device-resident solve --
