@@ -119,7 +119,21 @@ __device__ __forceinline__ uint32_t list_at_wave(const uint32_t* list, uint32_t 
 // every +-1 / +-pitch shift of them, fall on 32 distinct ds_read_b64 bank pairs
 // and 16 distinct ds_write_b64 banks per 16-lane group (pitch 10 was 2-way).
 constexpr int IP = 12;
-constexpr int IP16 = 20;  // 16x16 image pitch (18 + 2)
+// 16x16 image (kernel 5): row r of a wave's tile image (r = -1 .. 16, the halo
+// rows included) starts at slot img16_row(r), and cell (r, c), c = -1 .. 16, sits
+// at img16_row(r) + c.  The rows are skewed -- consecutive bases 32, 34, 32, 46
+// slots apart -- so that with lane (r = lane>>2, q = lane&3) owning columns
+// 4q..4q+3 of row r, every ds_read_b64 of a half-sweep (W, E, N, S of the
+// lane's two same-colour cells) lands its 32 lanes on 32 distinct bank pairs and
+// every ds_write_b64 its 16-lane groups on distinct banks.  With a constant
+// pitch the colour offset (r & 1) leaves only two bank classes per row
+// parity: the former pitch-20 image had every read and write 2-way
+// (PMC SQ_LDS_BANK_CONFLICT 3.7 G cycles per 16384^2 solve, more than the LDS
+// instructions' own 1.9 G).
+__device__ __forceinline__ int img16_row(int r) {
+  return 47 + 144 * (r >> 2) + 32 * (r & 3) + 2 * ((r >> 1) & 1);
+}
+constexpr int IMG16 = 640;  // img16_row(16) + 17
 
 // v_min_f64 on operands that are never NaN (T >= 0 or +inf): one instruction,
 // no canonicalisation (the compiler cannot prove no-NaN for fmin).
@@ -577,14 +591,16 @@ __device__ __forceinline__ int visit8(const PassArgs& a, double* img, unsigned l
 // running one after the other behind per-cell branches.  Same operations as
 // rb_update: bit-identical results (a discarded two-sided candidate may be
 // NaN from a negative radicand; it is never selected).
-template <bool FAST, int PITCH, bool APPROX = false>
-__device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, double f0,
-                                           double f1, double& t0, double& t1, bool& ch0,
-                                           bool& ch1) {
-  // all eight neighbour reads in flight before the first use
-  double w0 = img[s0 - 1], e0 = img[s0 + 1], n0 = img[s0 + PITCH], so0 = img[s0 - PITCH];
-  double w1 = img[s1 - 1], e1 = img[s1 + 1], n1 = img[s1 + PITCH], so1 = img[s1 - PITCH];
-  // one wait for all eight (the v_min asm below would otherwise pin reads behind it)
+template <bool FAST, bool APPROX = false>
+__device__ __forceinline__ void rb_update2(const double* p, const double* pn, const double* ps,
+                                           double f0, double f1, double& t0, double& t1,
+                                           bool& ch0, bool& ch1) {
+  // p: the lane's first cell of this colour (the second is p + 2, same row);
+  // pn / ps: the same column in the rows above / below (skewed image rows).
+  // All neighbour reads in flight before the first use (cell 1's W is cell 0's E).
+  double w0 = p[-1], e0 = p[1], n0 = pn[0], so0 = ps[0];
+  double w1 = p[1], e1 = p[3], n1 = pn[2], so1 = ps[2];
+  // one wait for all of them (the v_min asm below would otherwise pin reads behind it)
   asm volatile("" : "+v"(w0), "+v"(e0), "+v"(n0), "+v"(so0), "+v"(w1), "+v"(e1), "+v"(n1),
                "+v"(so1));
   // No skip test: u < t alone decides (u >= min + C/sqrt(2) > min + 0.7071 C, so
@@ -624,11 +640,14 @@ __device__ __forceinline__ void rb_update2(const double* img, int s0, int s1, do
   }
 }
 
+// pr / pb: the lane's first red / black cell in the image; dn / ds: slots to the
+// same column one row up / down (the lane's row and its neighbours, img16_row)
 template <bool FAST, bool APPROX = false>
-__device__ __forceinline__ int rb_sweeps4(double* img, const int (&sr)[2], const int (&sb)[2],
+__device__ __forceinline__ int rb_sweeps4(double* pr, double* pb, int dn, int ds,
                                           const double (&fr)[2], const double (&fb)[2],
                                           double (&tr)[2], double (&tb)[2], int max_inner,
                                           bool& capped, unsigned long long stop_at = ~0ull) {
+  const double *prn = pr + dn, *prs = pr - ds, *pbn = pb + dn, *pbs = pb - ds;
   int sweeps = 0;
   capped = true;
   // past stop_at (the pass deadline) a visit ends as if capped -- but only after
@@ -638,22 +657,22 @@ __device__ __forceinline__ int rb_sweeps4(double* img, const int (&sr)[2], const
     // two sweeps per convergence test: the second sweep's flags decide (a sweep
     // that changes nothing is the local fixed point)
     __builtin_amdgcn_wave_barrier();
-    rb_update2<FAST, IP16, APPROX>(img, sr[0], sr[1], fr[0], fr[1], tr[0], tr[1], i0, i1);
-    img[sr[0]] = tr[0];
-    img[sr[1]] = tr[1];
+    rb_update2<FAST, APPROX>(pr, prn, prs, fr[0], fr[1], tr[0], tr[1], i0, i1);
+    pr[0] = tr[0];
+    pr[2] = tr[1];
     __builtin_amdgcn_wave_barrier();
-    rb_update2<FAST, IP16, APPROX>(img, sb[0], sb[1], fb[0], fb[1], tb[0], tb[1], i2, i3);
-    img[sb[0]] = tb[0];
-    img[sb[1]] = tb[1];
+    rb_update2<FAST, APPROX>(pb, pbn, pbs, fb[0], fb[1], tb[0], tb[1], i2, i3);
+    pb[0] = tb[0];
+    pb[2] = tb[1];
     ++sweeps;
     __builtin_amdgcn_wave_barrier();
-    rb_update2<FAST, IP16, APPROX>(img, sr[0], sr[1], fr[0], fr[1], tr[0], tr[1], i0, i1);
-    img[sr[0]] = tr[0];
-    img[sr[1]] = tr[1];
+    rb_update2<FAST, APPROX>(pr, prn, prs, fr[0], fr[1], tr[0], tr[1], i0, i1);
+    pr[0] = tr[0];
+    pr[2] = tr[1];
     __builtin_amdgcn_wave_barrier();
-    rb_update2<FAST, IP16, APPROX>(img, sb[0], sb[1], fb[0], fb[1], tb[0], tb[1], i2, i3);
-    img[sb[0]] = tb[0];
-    img[sb[1]] = tb[1];
+    rb_update2<FAST, APPROX>(pb, pbn, pbs, fb[0], fb[1], tb[0], tb[1], i2, i3);
+    pb[0] = tb[0];
+    pb[2] = tb[1];
     ++sweeps;
     if (!__any(i0 || i1 || i2 || i3)) {
       capped = false;
@@ -678,9 +697,10 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
   const int r = lane >> 2, q = lane & 3, odd = r & 1;
   const int cr[2] = {4 * q + odd, 4 * q + 2 + odd};
   const int cb[2] = {4 * q + 1 - odd, 4 * q + 3 - odd};
-  const int row = (r + 1) * IP16;
-  const int sr[2] = {row + cr[0] + 1, row + cr[1] + 1};
-  const int sb[2] = {row + cb[0] + 1, row + cb[1] + 1};
+  const int rb = img16_row(r);  // slot of (r, 0); the halo columns are rb - 1, rb + 16
+  const int dn = img16_row(r + 1) - rb, ds = rb - img16_row(r - 1);
+  const int sr[2] = {rb + cr[0], rb + cr[1]};
+  const int sb[2] = {rb + cb[0], rb + cb[1]};
   const int64_t i0 = (int64_t)tx * TT, j0 = (int64_t)ty * TT;
   const int64_t gj = j0 + r;
   const bool rowin = has && gj < a.ny;
@@ -750,15 +770,15 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
   }
   asm volatile("" ::: "memory");  // the loads above issue before the gate's wait
   if (!gate()) return -1;
-  if (q == 0) img[row] = hw;
-  if (q == 3) img[row + TT + 1] = he;
+  if (q == 0) img[rb - 1] = hw;
+  if (q == 3) img[rb + TT] = he;
   if (r == 0) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) img[1 + 4 * q + k] = hs[k];
+    for (int k = 0; k < 4; ++k) img[img16_row(-1) + 4 * q + k] = hs[k];
   }
   if (r == TT - 1) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) img[(TT + 1) * IP16 + 1 + 4 * q + k] = hn[k];
+    for (int k = 0; k < 4; ++k) img[img16_row(TT) + 4 * q + k] = hn[k];
   }
   img[sb[0]] = tb[0];
   img[sb[1]] = tb[1];
@@ -766,8 +786,10 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
   const bool fast = __all(!(fr[0] < kFastMinF) && !(fr[1] < kFastMinF) &&
                           !(fb[0] < kFastMinF) && !(fb[1] < kFastMinF));
   const int sweeps =
-      fast ? rb_sweeps4<true, APPROX>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped, stop_at)
-           : rb_sweeps4<false>(img, sr, sb, fr, fb, tr, tb, a.max_inner, capped, stop_at);
+      fast ? rb_sweeps4<true, APPROX>(img + sr[0], img + sb[0], dn, ds, fr, fb, tr, tb,
+                                      a.max_inner, capped, stop_at)
+           : rb_sweeps4<false>(img + sr[0], img + sb[0], dn, ds, fr, fb, tr, tb, a.max_inner,
+                               capped, stop_at);
   // write back decreased cells; dr/db: the decreased value or +inf.  Keys are
   // non-negative doubles, so the u64 order of their bits (ek) is their f64
   // order and the edge minima below are v_min_f64 / v_cmp_f64 work.
@@ -784,14 +806,14 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
   // the halo snapshot across the edge, re-read from the image
   auto across = [&](double v, double hx) { return (!a.prune || v < hx) ? v : dinf(); };
   if (r == 0 || r == TT - 1) {  // S / N edge: rows 0 and 15 (disjoint lanes), halo row beyond
-    const int vo = r == 0 ? -IP16 : IP16;
+    const int vo = r == 0 ? -ds : dn;
     const double m = vmin64(vmin64(across(dr[0], img[sr[0] + vo]), across(dr[1], img[sr[1] + vo])),
                             vmin64(across(db[0], img[sb[0] + vo]), across(db[1], img[sb[1] + vo])));
     if (m < dinf()) atomicMin(&ek[r == 0 ? 0 : 3], dbits(m));
   }
   if (q == 0 || q == 3) {  // W / E edge: column 0 (cr[0] or cb[0]) / column 15 (cr[1] or cb[1])
     const double c = q == 0 ? (odd ? db[0] : dr[0]) : (odd ? dr[1] : db[1]);
-    const double m = across(c, img[q == 0 ? row : row + TT + 1]);
+    const double m = across(c, img[q == 0 ? rb - 1 : rb + TT]);
     if (m < dinf()) atomicMin(&ek[q == 0 ? 1 : 2], dbits(m));
   }
   return sweeps;
@@ -805,7 +827,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_prio(PassArgs a) {
   static_assert(TS == 8, "kernel 4: 8x8 tiles (16x16 tiles are kernel 5, k_fim_pass_dyn)");
   constexpr int TPW = TS == 8 ? 2 : 1;  // tiles per wave
   constexpr int SLOTS = WPB * TPW;       // tile slots per workgroup
-  constexpr int IMG = TS == 8 ? (WT + 2) * IP : (16 + 2) * IP16;
+  constexpr int IMG = (WT + 2) * IP;
   __shared__ uint32_t s_q[QCAP];
   __shared__ uint32_t s_work[WCAP];
   __shared__ unsigned long long s_wkey[WCAP];
@@ -1013,7 +1035,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_prio(PassArgs a) {
 // converging tile moves on to the next entry while the others still sweep.
 template <int WPB, bool APPROX>
 __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
-  constexpr int IMG = (16 + 2) * IP16;
+  constexpr int IMG = IMG16;
   __shared__ uint32_t s_q[QCAP];
   __shared__ uint32_t s_pref[kShards + 1];
   __shared__ uint32_t s_hout[kBins];

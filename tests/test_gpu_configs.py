@@ -112,14 +112,21 @@ def test_config5_hazard_window_4096(terrain4096, oracle):
     sub[inner] = np.minimum(1.0, sub[inner] + 1.0)
     sub[ring] = np.minimum(1.0, sub[ring] + 0.1)
     i0, j0, w = c[0] - r - 1, c[1] - r - 1, 2 * r + 3
-    for target in (hd, hd0):  # the bump (speed up), then cleared again (speed down)
+    # the bump (speeds up: theta reset), then cleared again (speeds down: the
+    # decrease-only update, no reset), each vs the oracle FMM of the new speed
+    visits = []
+    for target, dec in ((hd, False), (hd0, True)):
         t.eng.h2d(t.st["hazard"], target)
         t.eng.pack_speed(N, N, N, 1.0, t.st, t.dF)
-        sw = t.eng.resolve_window_device(t.dF, t.dT, N, N, N, goal[0], goal[1], i0, j0, w, w)
+        sw = t.eng.update_window_device(t.dF, t.dT, N, N, N, goal[0], goal[1], i0, j0, w, w,
+                                        decrease_only=dec)
         F = t.get(t.dF)
         Tref, _ = oracle.fmm(F, goal)
         _parity(t.get(t.dT), Tref)
         assert sw["passes"] > 0
+        visits.append(sw["tile_visits"])
+    cold = t.eng.solve_device(t.dF, t.dT, N, N, N, *goal)
+    assert visits[1] < visits[0] < cold["tile_visits"]
 
 
 def test_config4_32768_eight_slabs(dymu):

@@ -325,3 +325,37 @@ def test_incremental_resolve_through_planner(dymu, oracle):
     assert p.setGoal((40, 160))
     p.computeEntireTotalCostMap()
     assert p.lastSolveKind() == 0
+
+
+@pytest.mark.gpu
+def test_decrease_only_window_through_planner(dymu, oracle):
+    """C = res*cost*(2+hd-tr) grows when the trafficability drops (the local
+    layer's write on a replaced segment, LocalPathRepairing.cpp:389-394): an
+    increase, re-propagated with the theta reset; restoring it is a decrease,
+    re-propagated without any reset.  Both through the windowed setter; each
+    result equals the oracle FMM of the new speed."""
+    N = 160
+    F = oracle.synth_speed(N, N, seed=17, obst_frac=0.02, obst_seed=19, goal=(120, 30))
+    cost = np.where(np.isfinite(F), F, -1.0)
+    p = dymu.Planner()
+    p.initGlobalLayer(1.0, 0.5, N, N)
+    p.setCostMap(cost)
+    assert p.setGoal((120, 30))
+    p.computeEntireTotalCostMap()
+    win = (40, 90, 12, 9)  # i0, j0, w, h
+    i0, j0, w, h = win
+    obst = ~np.isfinite(F)
+    visits = {}
+    for name, tr_val in (("up", 0.25), ("down", 1.0)):  # tr drop raises C; restoring lowers it
+        assert p.setTrafficabilityWindow(i0, j0, np.full((h, w), tr_val))
+        p.computeEntireTotalCostMap()
+        assert p.lastSolveKind() == 1
+        visits[name] = p.lastStats()["tile_visits"]
+        Fr = oracle.pack_speed(cost, p.getHazardDensityMatrix(), p.getTrafficabilityMatrix(),
+                               obst, res=1.0)
+        Tref, _ = oracle.fmm(Fr, (120, 30))
+        T = p.totalCostRaw()
+        assert np.array_equal(np.isinf(T), np.isinf(Tref))
+        fin = np.isfinite(Tref)
+        assert (np.abs(T[fin] - Tref[fin]) / np.maximum(1, Tref[fin])).max() <= RTOL
+    assert visits["down"] <= visits["up"]

@@ -71,6 +71,7 @@ def main(N=4096, reps=5):
     r = 20
     hd = np.zeros((N, N))
     eng.d2h(hd, st["hazard"])
+    hd0 = hd.copy()
     jj, ii = np.mgrid[c[1] - r - 1:c[1] + r + 2, c[0] - r - 1:c[0] + r + 2]
     d2 = (ii - c[0]) ** 2 + (jj - c[1]) ** 2
     sub = hd[c[1] - r - 1:c[1] + r + 2, c[0] - r - 1:c[0] + r + 2]
@@ -96,6 +97,38 @@ def main(N=4096, reps=5):
         tcold.append(sc["ms"])
     Tc = np.empty((N, N))
     eng.d2h(Tc, dT)
+    # the disc cleared again: a decrease-only change (no reset, window tiles seeded)
+    eng.h2d(st["hazard"], hd0)
+    eng.pack_speed(N, N, N, 1.0, st, dF)
+    eng.solve_device(dF, dT0, N, N, N, *goal)
+    T0c = np.empty((N, N))
+    eng.d2h(T0c, dT0)  # reference point: the cold solve of the cleared speed
+    eng.h2d(st["hazard"], hd)
+    eng.pack_speed(N, N, N, 1.0, st, dF)
+    eng.solve_device(dF, dT0, N, N, N, *goal)
+    Tb = np.empty((N, N))
+    eng.d2h(Tb, dT0)  # converged map with the disc
+    eng.h2d(st["hazard"], hd0)
+    eng.pack_speed(N, N, N, 1.0, st, dF)
+    td, sd = [], None
+    for _ in range(reps):
+        eng.h2d(dT, Tb)
+        sd = eng.update_window_device(dF, dT, N, N, N, goal[0], goal[1], i0, j0, w, w, True)
+        td.append(sd["ms"])
+    Td = np.empty((N, N))
+    eng.d2h(Td, dT)
+    tcold2 = []
+    for _ in range(reps):
+        tcold2.append(eng.solve_device(dF, dT, N, N, N, *goal)["ms"])
+    fin0 = np.isfinite(T0c)
+    out["config5_clear"] = {
+        "decrease_only_ms": float(np.median(td)), "cold_ms": float(np.median(tcold2)),
+        "speedup": float(np.median(tcold2) / np.median(td)),
+        "decrease_only_tile_visits": sd["tile_visits"], "passes": sd["passes"],
+        "inf_mask_equal": bool(np.array_equal(np.isinf(Td), np.isinf(T0c))),
+        "max_rel_diff_vs_cold": float((np.abs(Td[fin0] - T0c[fin0]) /
+                                       np.maximum(1, T0c[fin0])).max()),
+    }
     fin = np.isfinite(Tc)
     out["config5"] = {
         "window": [i0, j0, w, w], "windowed_ms": float(np.median(tw)),
