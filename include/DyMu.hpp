@@ -14,10 +14,16 @@
 //   getPath / computeGlobalPath :589-662 (+ :666-784)
 //   getTotalCostMatrix, getGlobalCostMatrix, getHazardDensityMatrix,
 //   getTrafficabilityMatrix, getTotalCost, getLocomotionMode  :788-890
+//   local layer (src/DyMu_LocalPathRepairing.cpp, csrc/local_layer.cpp):
+//   computeLocalPlanning, repairPath, evaluatePath, expandRisk,
+//   computeLocalPropagation, getLocalPath, computeLocalWaypointGDM,
+//   getRiskMatrix, getDeviationMatrix, getReconnectingIndex, getLocalNode,
+//   subdivideGlobalNode, getTotalCost(localNode)
 // Differences a caller can see:
-//   * the local (sub-grid) layer, CoRa and risk methods are not part of this
-//     library (out of scope); getPath's evaluatePath(0) is then the
-//     identity, as in the reference when no local map exists.
+//   * nodes are SoA arrays, not heap records: getGlobalNode /
+//     getNearestGlobalNode / getLocalNode return snapshots (std::optional for
+//     the reference's NULL), node-taking methods take grid indices or a
+//     snapshot; CoRa (cost-ratio learning) is not part of this library.
 //   * computeTotalCostMap stops like the reference once the start and its nb4
 //     are final: CLOSED cells hold their converged values, the
 //     narrow band the reference's tentative values (replayed on the host from
@@ -30,6 +36,8 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
+#include <optional>
 #include <string>
 #include <vector>
 
@@ -44,6 +52,37 @@ enum repairingAproach {
   CONSERVATIVE,  // Hazard Avoidance - FM*
   SWEEPING       // multiBiFM*
 };
+
+// Snapshot of a global node (the reference's globalNode, src/DyMu.hpp:69-108,
+// without the neighbour pointer lists and the local map).
+struct globalNode {
+  base::Pose2D pose;        // grid indices (i, j)
+  base::Pose2D world_pose;  // i * res, j * res
+  double elevation = 0.0, slope = 0.0;
+  node_state state = OPEN;
+  bool isObstacle = false;
+  bool hasLocalMap = false;
+  double raw_cost = 0.0, cost = 0.0, hazard_density = 0.0, trafficability = 1.0;
+  double total_cost = 0.0;
+  unsigned terrain = 0;
+  std::string nodeLocMode = "DONT_CARE";
+};
+
+// Snapshot of a local-layer sub-cell (the reference's localNode,
+// src/DyMu.hpp:42-67, without nb4List).  id names the sub-cell for the
+// node-taking methods below.
+struct localNode {
+  base::Pose2D pose;         // sub-cell indices inside the parent global node
+  base::Pose2D world_pose;   // global_pose / global_res
+  base::Pose2D parent_pose;  // parent global node (grid indices)
+  base::Pose2D global_pose;  // in global units
+  double deviation = 0.0, total_cost = 0.0, cost = 0.0, risk = 0.0;
+  node_state state = OPEN;
+  bool isObstacle = false;
+  uint64_t id = 0;
+};
+
+struct LocalLayer;  // csrc/local_layer.cpp
 
 class DyMuPathPlanner {
  public:
@@ -83,6 +122,35 @@ class DyMuPathPlanner {
   std::vector<std::vector<double>> getTrafficabilityMatrix();
   double getTotalCost(base::Waypoint wInt);
 
+  // -- node-level access (src/DyMu.hpp:500-518); std::nullopt = the reference's NULL --
+  std::optional<globalNode> getGlobalNode(unsigned i, unsigned j);
+  std::optional<globalNode> getNearestGlobalNode(base::Pose2D pos);
+  std::optional<globalNode> getNearestGlobalNode(base::Waypoint wPos);
+  std::optional<globalNode> globalGoal();  // the reference's public global_goal
+  bool isSafeNode(unsigned i, unsigned j);         // :410-422 (border -> false)
+  bool isFullyClosedNode(unsigned i, unsigned j);  // :424-436 (border -> false)
+  void resetTotalCostMap();                        // :473-485: every node OPEN at +inf
+
+  // -- local layer (src/DyMu.hpp:539-591) --
+  bool computeLocalPlanning(base::Waypoint wPos, base::samples::frame::Frame traversabilityMap,
+                            double res, std::vector<base::Waypoint>& trajectory,
+                            base::Time& localTime);
+  int repairPath(base::Waypoint wInit, unsigned index);
+  bool evaluatePath(unsigned starting_index);
+  void expandRisk();
+  // the set node, or std::nullopt (the reference's NULL)
+  std::optional<localNode> computeLocalPropagation(base::Waypoint wInit, base::Waypoint wOvertake);
+  std::vector<base::Waypoint> getLocalPath(const localNode& lSetNode, base::Waypoint wInit,
+                                           double tau);
+  bool computeLocalWaypointGDM(base::Waypoint& wPos, double tau);
+  std::optional<localNode> getLocalNode(base::Waypoint wPos);  // subdivides, like :177-189
+  std::optional<localNode> getLocalNode(base::Pose2D pos);     // :160-173
+  void subdivideGlobalNode(unsigned i, unsigned j);            // :150-156
+  double getTotalCost(const localNode& lNode);                 // :473-491
+  std::vector<std::vector<double>> getRiskMatrix(base::Waypoint rover_pos);
+  std::vector<std::vector<double>> getDeviationMatrix(base::Waypoint rover_pos);
+  int getReconnectingIndex();
+
   // -- extensions (not in the reference) --
   // Flat row-major views for FFI callers (ny*nx, index j*nx + i).  The total
   // cost lives on the device; this downloads whatever the host copy lacks.
@@ -111,6 +179,18 @@ class DyMuPathPlanner {
   uint64_t lastBandSize() const { return band_size_; }
   // Engine options (device ordinal etc.); takes effect on the next solve.
   void setEngineOptions(const dymu_opts& o);
+  // Install a total-cost map (ny*nx, +inf unreachable) as the state a
+  // converged computeEntireTotalCostMap leaves: every finite node CLOSED (the
+  // reference's public globalNode::total_cost / state writes).  The next
+  // solve starts cold.  No solve runs here.
+  bool loadTotalCostMap(const double* T);
+  // local-layer inspection: how many global nodes are subdivided (mask: ny*nx
+  // bytes, may be null), and one subdivided node's sub-cells (r*r each,
+  // row-major) -- false if (i, j) has no local map
+  uint64_t localMapMask(uint8_t* mask) const;
+  bool localBlock(unsigned i, unsigned j, double* dev, double* tc, double* risk, uint8_t* state,
+                  uint8_t* obst) const;
+  unsigned resRatio() const { return res_ratio_; }
 
  private:
   uint64_t idx(unsigned i, unsigned j) const { return (uint64_t)j * nx_ + i; }
@@ -129,7 +209,17 @@ class DyMuPathPlanner {
   bool propagate(bool early, unsigned si, unsigned sj);
   void replayBand(double t_closed, const std::vector<uint64_t>& band, std::vector<double>& out);
   void gradientNode(unsigned i, unsigned j, double& dnx, double& dny) const;
-  bool isSafeNode(unsigned i, unsigned j) const;
+  bool safeNode(unsigned i, unsigned j) const;
+  std::optional<globalNode> snapshot(uint64_t k);
+  // local layer internals (csrc/local_layer.cpp)
+  int64_t nearestIndex(double x, double y) const;
+  uint64_t localCell(uint64_t p, localNode* out) const;
+  int64_t localAt(double x, double y);  // getLocalNode by sub-cell id, -1 = NULL
+  double localTotalCost(uint64_t p) const;
+  bool isBlockingObstacle(uint64_t p, unsigned& maxIndex, unsigned& minIndex) const;
+  int64_t localPropagation(base::Waypoint wInit, base::Waypoint wOvertake);
+  std::vector<base::Waypoint> localPath(uint64_t set, base::Waypoint wInit);
+  void windowMatrix(base::Waypoint rover_pos, bool deviation, std::vector<std::vector<double>>& m);
 
   static constexpr unsigned kBlk = 128;
 
@@ -138,6 +228,8 @@ class DyMuPathPlanner {
   repairingAproach repairing_approach_;
   unsigned nx_ = 0, ny_ = 0;
   double global_res_ = 1.0, local_res_ = 1.0;
+  unsigned res_ratio_ = 1;
+  std::unique_ptr<LocalLayer> local_;
   std::vector<double> global_offset_{0.0, 0.0};
   std::vector<double> slope_range_;
   std::vector<std::string> locomotion_modes_;

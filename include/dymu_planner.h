@@ -80,6 +80,59 @@ int dymu_planner_last_stats(dymu_planner* p, dymu_stats* out);
  * where the speed changed (dymu_resolve_window), 2 previous map reused */
 int dymu_planner_last_solve_kind(dymu_planner* p);
 
+/* ---- node-level access (src/DyMu.hpp:500-518, extension of the flat ABI) ---- */
+typedef struct dymu_global_node {
+  double elevation, slope, raw_cost, cost, hazard_density, trafficability, total_cost;
+  uint32_t terrain;
+  int32_t state;        /* 0 OPEN, 1 CLOSED */
+  int32_t is_obstacle;
+  int32_t has_local_map;
+} dymu_global_node;
+/* getGlobalNode (:313-317): 1 and *out, or 0 (NULL) */
+int dymu_planner_get_global_node(dymu_planner* p, uint32_t i, uint32_t j, dymu_global_node* out);
+int dymu_planner_is_safe_node(dymu_planner* p, uint32_t i, uint32_t j);          /* :410-422 */
+int dymu_planner_is_fully_closed_node(dymu_planner* p, uint32_t i, uint32_t j);  /* :424-436 */
+int dymu_planner_reset_total_cost_map(dymu_planner* p);                          /* :473-485 */
+/* install a total-cost map (ny*nx, +inf unreachable) as a converged
+ * computeEntireTotalCostMap leaves it (every finite node CLOSED) */
+int dymu_planner_load_total_cost_map(dymu_planner* p, const double* T);
+/* current_path (public member, src/DyMu.hpp:456): n waypoints (x, y, z, heading) */
+int dymu_planner_set_current_path(dymu_planner* p, const double* xyzh, int n);
+int dymu_planner_get_current_path(dymu_planner* p, double* out_xyzh, int max_wp);
+
+/* ---- local layer (src/DyMu_LocalPathRepairing.cpp) ---- */
+/* computeLocalPlanning (:193-291).  image: height rows of row_size bytes, pixel
+ * (i, j) at image[j*row_size + i*pixel_size], nonzero = obstacle.  Returns 1
+ * when the path was repaired (trajectory = current_path, *n_traj waypoints, at
+ * most max_traj written; *local_time_s = repair time), 0 when not blocked. */
+int dymu_planner_compute_local_planning(dymu_planner* p, double x, double y, double z,
+                                        double heading, const uint8_t* image, uint32_t width,
+                                        uint32_t height, uint32_t row_size, uint32_t pixel_size,
+                                        double res, double* traj_xyzh, int max_traj,
+                                        int* n_traj, double* local_time_s);
+/* repairPath (:298-435): the reconnecting index or -1 */
+int dymu_planner_repair_path(dymu_planner* p, double x, double y, double z, double heading,
+                             uint32_t index);
+/* evaluatePath (:1027-1109) */
+int dymu_planner_evaluate_path(dymu_planner* p, uint32_t starting_index);
+/* expandRisk (:493-523) */
+int dymu_planner_expand_risk(dymu_planner* p);
+/* computeLocalPropagation (:578-698): 1 and the set node's global pose, or 0 (NULL) */
+int dymu_planner_compute_local_propagation(dymu_planner* p, const double* start_xyzh,
+                                           const double* overtake_xyzh, double* set_xy);
+/* getRiskMatrix / getDeviationMatrix (:1111-1211): (21*r)^2 doubles, r = res ratio */
+int dymu_planner_get_risk_matrix(dymu_planner* p, double x, double y, double z, double heading,
+                                 double* out);
+int dymu_planner_get_deviation_matrix(dymu_planner* p, double x, double y, double z,
+                                      double heading, double* out);
+int dymu_planner_get_reconnecting_index(dymu_planner* p);
+int dymu_planner_res_ratio(dymu_planner* p);
+/* subdivided global nodes: count, and a ny*nx byte mask (may be NULL) */
+int64_t dymu_planner_local_map_mask(dymu_planner* p, uint8_t* mask);
+/* one subdivided node's r*r sub-cells ([j][i]); 0 if (i, j) has no local map */
+int dymu_planner_local_block(dymu_planner* p, uint32_t i, uint32_t j, double* dev, double* tc,
+                             double* risk, uint8_t* state, uint8_t* obst);
+
 #ifdef __cplusplus
 }
 #endif

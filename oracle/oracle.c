@@ -582,27 +582,48 @@ static int push_wp(double* out, int* n, int max_wp, wp_t w) {
   return 1;
 }
 
-int oracle_global_path(const double* T, const double* elev, uint32_t nx, uint32_t ny, double res,
-                       uint32_t gi, uint32_t gj, double goal_heading, double risk_distance,
-                       double wx, double wy, double wh, double* wp, int max_wp) {
+/* :615-662.  Returns 1 (true), 0 (false at :628-633 or :650-656: the
+ * waypoints pushed so far are kept, as current_path keeps them), -3 when more
+ * than max_wp waypoints would be produced; *n_out = #waypoints written. */
+int oracle_global_path_partial(const double* T, const double* elev, uint32_t nx, uint32_t ny,
+                               double res, uint32_t gi, uint32_t gj, double goal_heading,
+                               double risk_distance, double wx, double wy, double wh, double* wp,
+                               int max_wp, int* n_out) {
   wp_t sink = {res * (double)gi, res * (double)gj, elev ? elev[(uint64_t)gj * nx + gi] : 0,
                goal_heading};
   wp_t pos = {wx, wy, 0, wh};
   int n = 0;
+  *n_out = 0;
   double tau = 0.4 < risk_distance ? 0.4 : risk_distance; /* std::min(0.4, rd) */
   wp_t nxt = next_waypoint(T, elev, nx, ny, res, &pos, tau);
-  if (isnan(nxt.x) || isnan(nxt.y)) return -1; /* :628-633 */
+  if (isnan(nxt.x) || isnan(nxt.y)) return 0; /* :628-633 */
   if (!push_wp(wp, &n, max_wp, pos)) return -3;
   pos = nxt;
   while (sqrt((pos.x - sink.x) * (pos.x - sink.x) + (pos.y - sink.y) * (pos.y - sink.y)) >
          2.0 * res) {
     nxt = next_waypoint(T, elev, nx, ny, res, &pos, tau);
     if (!push_wp(wp, &n, max_wp, pos)) return -3;
+    *n_out = n;
     if (sqrt((pos.x - nxt.x) * (pos.x - nxt.x) + (pos.y - nxt.y) * (pos.y - nxt.y)) <
         0.01 * tau * res)
-      return -2; /* :650-656 */
+      return 0; /* :650-656 */
     pos = nxt;
   }
   if (!push_wp(wp, &n, max_wp, sink)) return -3;
-  return n;
+  *n_out = n;
+  return 1;
+}
+
+int oracle_global_path(const double* T, const double* elev, uint32_t nx, uint32_t ny, double res,
+                       uint32_t gi, uint32_t gj, double goal_heading, double risk_distance,
+                       double wx, double wy, double wh, double* wp, int max_wp) {
+  int n = 0;
+  wp_t probe = {wx, wy, 0, wh};
+  double tau = 0.4 < risk_distance ? 0.4 : risk_distance;
+  wp_t nxt = next_waypoint(T, elev, nx, ny, res, &probe, tau);
+  if (isnan(nxt.x) || isnan(nxt.y)) return -1;
+  int st = oracle_global_path_partial(T, elev, nx, ny, res, gi, gj, goal_heading, risk_distance,
+                                      wx, wy, wh, wp, max_wp, &n);
+  if (st == -3) return -3;
+  return st == 1 ? n : -2;
 }

@@ -110,6 +110,40 @@ int oracle_global_path(const double* T, const double* elev, uint32_t nx, uint32_
                        uint32_t gi, uint32_t gj, double goal_heading, double risk_distance,
                        double wx, double wy, double wh, double* wp, int max_wp);
 
+/* computeGlobalPath keeping what it pushed before a failure (see oracle.c). */
+int oracle_global_path_partial(const double* T, const double* elev, uint32_t nx, uint32_t ny,
+                               double res, uint32_t gi, uint32_t gj, double goal_heading,
+                               double risk_distance, double wx, double wy, double wh, double* wp,
+                               int max_wp, int* n_out);
+
+/* ---- the local layer (oracle_local.c; reference DyMu_LocalPathRepairing.cpp) ----
+ * A context holds a copy of the global layer the local layer reads (obstacle
+ * flags, total cost, CLOSED state, elevation, goal) and writes (hazard
+ * density, trafficability), current_path and the lazily subdivided sub-grid. */
+typedef struct oracle_local oracle_local;
+oracle_local* oracle_local_create(uint32_t nx, uint32_t ny, double gres, double lres, double offx,
+                                  double offy, double risk_distance, double reconnect_distance,
+                                  double risk_ratio, int approach);
+void oracle_local_destroy(oracle_local* L);
+/* any pointer may be NULL (keeps the current array) */
+void oracle_local_set_global(oracle_local* L, const uint8_t* obst, const double* T,
+                             const uint8_t* closed, const double* elev, const double* hazard,
+                             const double* traff, uint32_t gi, uint32_t gj, double goal_heading);
+void oracle_local_get_global(const oracle_local* L, double* hazard, double* traff);
+void oracle_local_set_path(oracle_local* L, const double* wp, int n);
+int oracle_local_get_path(const oracle_local* L, double* wp, int max_wp);
+int oracle_local_reconnecting_index(const oracle_local* L);
+int oracle_local_planning(oracle_local* L, double x, double y, double z, double h,
+                          const uint8_t* image, uint32_t width, uint32_t height,
+                          uint32_t row_size, uint32_t pixel_size, double res);
+int oracle_local_get_path_eval(oracle_local* L, double x, double y, double z, double h,
+                               double* wp, int max_wp);
+void oracle_local_risk_matrix(oracle_local* L, double x, double y, double* out);
+void oracle_local_deviation_matrix(oracle_local* L, double x, double y, double* out);
+uint64_t oracle_local_map_mask(const oracle_local* L, uint8_t* mask);
+int oracle_local_block(const oracle_local* L, uint32_t gi, uint32_t gj, double* dev, double* tc,
+                       double* risk, uint8_t* state, uint8_t* obst);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,6 +20,7 @@
 #include <unordered_map>
 
 #include "DyMu.hpp"
+#include "local_layer.hpp"
 
 namespace PathPlanning_lib {
 
@@ -71,6 +72,13 @@ bool DyMuPathPlanner::initGlobalLayer(double globalres, double localres, unsigne
                                       unsigned num_nodes_Y, std::vector<double> offset) {
   global_res_ = globalres;
   local_res_ = localres;
+  {
+    const double rr = global_res_ / local_res_;  // :49 res_ratio = (uint)(global_res / local_res)
+    res_ratio_ = (rr > -9.2e18 && rr < 9.2e18) ? (unsigned)(int64_t)rr : 0u;
+  }
+  if (!local_) local_ = std::make_unique<LocalLayer>();
+  local_->reset(res_ratio_);
+  reconnecting_index = 0;
   solved_ = false;
   nx_ = num_nodes_X;
   ny_ = num_nodes_Y;
@@ -608,7 +616,7 @@ bool DyMuPathPlanner::computeEntireTotalCostMap() {
 
 // :410-422 (start and its 8 neighbours must be free; border -> false here,
 // where the reference dereferences NULL)
-bool DyMuPathPlanner::isSafeNode(unsigned i, unsigned j) const {
+bool DyMuPathPlanner::safeNode(unsigned i, unsigned j) const {
   if (i == 0 || j == 0 || i + 1 >= nx_ || j + 1 >= ny_) return false;
   for (int dj = -1; dj <= 1; ++dj)
     for (int di = -1; di <= 1; ++di)
@@ -633,7 +641,7 @@ bool DyMuPathPlanner::computeTotalCostMap(base::Waypoint wPos) {
     return false;
   }
   const unsigned si = (unsigned)fx, sj = (unsigned)fy;
-  if (!isSafeNode(si, sj)) {
+  if (!safeNode(si, sj)) {
     log_error("PLANNER: The rover is located too close to an obstacle");
     return false;
   }
@@ -644,11 +652,13 @@ bool DyMuPathPlanner::computeTotalCostMap(base::Waypoint wPos) {
   return true;
 }
 
-// :589-611.  evaluatePath(0) is the identity without local maps.
+// :589-611 (evaluatePath(0) repairs the segments through local risk; it is the
+// identity while no global node is subdivided)
 std::vector<base::Waypoint> DyMuPathPlanner::getPath(base::Waypoint wPos) {
   wPos.position[0] -= global_offset_[0];
   wPos.position[1] -= global_offset_[1];
   computeGlobalPath(wPos);
+  evaluatePath(0);
   std::vector<base::Waypoint> out = current_path;
   for (auto& w : out) {
     w.position[0] += global_offset_[0];
@@ -807,7 +817,7 @@ double DyMuPathPlanner::getTotalCost(base::Waypoint wInt) {
   const double y = wInt.position[1] - global_offset_[1];
   const unsigned i = (unsigned)(x / global_res_), j = (unsigned)(y / global_res_);
   const double a = x - (double)i, b = y - (double)j;
-  if (i + 1 >= nx_ || j + 1 >= ny_) {  // a corner is NULL
+  if (i >= nx_ || j >= ny_ || i + 1 >= nx_ || j + 1 >= ny_) {  // a corner is NULL
     const unsigned ni = (unsigned)(x / global_res_ + 0.5), nj = (unsigned)(y / global_res_ + 0.5);
     if (ni >= nx_ || nj >= ny_) return kInf;
     return T(idx(ni, nj));
@@ -821,6 +831,92 @@ double DyMuPathPlanner::getTotalCost(base::Waypoint wInt) {
   const double w00 = T(k), w10 = T(k10);
   const double w01 = T(k01), w11 = T(k11);
   return w00 + (w10 - w00) * a + (w01 - w00) * b + (w11 + w00 - w10 - w01) * a * b;
+}
+
+// ---- node-level access (src/DyMu.hpp:500-518) ----
+
+std::optional<globalNode> DyMuPathPlanner::snapshot(uint64_t k) {
+  globalNode n;
+  const unsigned i = (unsigned)(k % nx_), j = (unsigned)(k / nx_);
+  n.pose.position[0] = (double)i;
+  n.pose.position[1] = (double)j;
+  if (has_goal_ && i == goal_i_ && j == goal_j_) n.pose.orientation = goal_heading_;
+  n.world_pose.position[0] = (double)i * global_res_;  // globalNode ctor (src/DyMu.hpp:92-93)
+  n.world_pose.position[1] = (double)j * global_res_;
+  n.elevation = elevation_[k];
+  n.slope = slope_[k];
+  n.state = closedCell(k) ? CLOSED : OPEN;
+  n.isObstacle = is_obstacle_[k] != 0;
+  n.hasLocalMap = local_ && local_->block(k) >= 0;
+  n.raw_cost = raw_cost_[k];
+  n.cost = cost_[k];
+  n.hazard_density = hazard_[k];
+  n.trafficability = traff_[k];
+  n.total_cost = T(k);
+  n.terrain = terrain_[k];
+  const int m = loc_mode_[k];
+  n.nodeLocMode = (m < 0 || m >= (int)locomotion_modes_.size()) ? "DONT_CARE" : locomotion_modes_[m];
+  return n;
+}
+
+// :313-317
+std::optional<globalNode> DyMuPathPlanner::getGlobalNode(unsigned i, unsigned j) {
+  if (i >= nx_ || j >= ny_) return std::nullopt;
+  return snapshot(idx(i, j));
+}
+
+// :570-584
+std::optional<globalNode> DyMuPathPlanner::getNearestGlobalNode(base::Pose2D pos) {
+  const int64_t k = nearestIndex(pos.position[0], pos.position[1]);
+  if (k < 0) return std::nullopt;
+  return snapshot((uint64_t)k);
+}
+
+std::optional<globalNode> DyMuPathPlanner::getNearestGlobalNode(base::Waypoint wPos) {
+  const int64_t k = nearestIndex(wPos.position[0], wPos.position[1]);
+  if (k < 0) return std::nullopt;
+  return snapshot((uint64_t)k);
+}
+
+std::optional<globalNode> DyMuPathPlanner::globalGoal() {
+  if (!has_goal_) return std::nullopt;
+  return snapshot(idx(goal_i_, goal_j_));
+}
+
+bool DyMuPathPlanner::isSafeNode(unsigned i, unsigned j) { return safeNode(i, j); }
+
+// :424-436 (a border node returns false where the reference dereferences NULL)
+bool DyMuPathPlanner::isFullyClosedNode(unsigned i, unsigned j) {
+  if (i == 0 || j == 0 || i + 1 >= nx_ || j + 1 >= ny_) return false;
+  const uint64_t k = idx(i, j);
+  return closedCell(k) && closedCell(k - nx_) && closedCell(k - 1) && closedCell(k + 1) &&
+         closedCell(k + nx_);
+}
+
+// :473-485
+void DyMuPathPlanner::resetTotalCostMap() {
+  std::fill(total_cost_.begin(), total_cost_.end(), kInf);
+  std::fill(blk_ok_.begin(), blk_ok_.end(), 1);
+  blk_missing_ = 0;
+  closed_limit_ = 0.0;
+  band_size_ = 0;
+  solved_ = false;
+}
+
+bool DyMuPathPlanner::loadTotalCostMap(const double* Tin) {
+  const uint64_t n = (uint64_t)nx_ * ny_;
+  if (!Tin || n == 0) return false;
+  std::memcpy(total_cost_.data(), Tin, sizeof(double) * n);
+  std::fill(blk_ok_.begin(), blk_ok_.end(), 1);
+  blk_missing_ = 0;
+  closed_limit_ = kInf;
+  band_size_ = 0;
+  solved_ = false;
+  if (ctx_ && dT_ && dcells_ == n &&
+      dymu_memcpy_h2d(ctx_, dT_, total_cost_.data(), sizeof(double) * n) != DYMU_OK)
+    throw std::runtime_error(std::string("dymu: total-cost upload failed: ") +
+                             dymu_last_error(ctx_));
+  return true;
 }
 
 }  // namespace PathPlanning_lib

@@ -225,4 +225,165 @@ int64_t dymu_planner_last_band_size(dymu_planner* p) {
   return (int64_t)p->pl.lastBandSize();
 }
 
+int dymu_planner_get_global_node(dymu_planner* p, uint32_t i, uint32_t j, dymu_global_node* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  return guarded([&] {
+    const auto n = p->pl.getGlobalNode(i, j);
+    if (!n) return 0;
+    out->elevation = n->elevation;
+    out->slope = n->slope;
+    out->raw_cost = n->raw_cost;
+    out->cost = n->cost;
+    out->hazard_density = n->hazard_density;
+    out->trafficability = n->trafficability;
+    out->total_cost = n->total_cost;
+    out->terrain = n->terrain;
+    out->state = n->state == PathPlanning_lib::CLOSED ? 1 : 0;
+    out->is_obstacle = n->isObstacle ? 1 : 0;
+    out->has_local_map = n->hasLocalMap ? 1 : 0;
+    return 1;
+  });
+}
+
+int dymu_planner_is_safe_node(dymu_planner* p, uint32_t i, uint32_t j) {
+  if (!p) return DYMU_ERR_ARG;
+  return guarded([&] { return (int)p->pl.isSafeNode(i, j); });
+}
+
+int dymu_planner_is_fully_closed_node(dymu_planner* p, uint32_t i, uint32_t j) {
+  if (!p) return DYMU_ERR_ARG;
+  return guarded([&] { return (int)p->pl.isFullyClosedNode(i, j); });
+}
+
+int dymu_planner_reset_total_cost_map(dymu_planner* p) {
+  if (!p) return DYMU_ERR_ARG;
+  p->pl.resetTotalCostMap();
+  return DYMU_OK;
+}
+
+int dymu_planner_load_total_cost_map(dymu_planner* p, const double* T) {
+  if (!p || !T) return DYMU_ERR_ARG;
+  return guarded([&] { return (int)p->pl.loadTotalCostMap(T); });
+}
+
+int dymu_planner_set_current_path(dymu_planner* p, const double* xyzh, int n) {
+  if (!p || n < 0 || (n > 0 && !xyzh)) return DYMU_ERR_ARG;
+  return guarded([&] {
+    p->pl.current_path.clear();
+    for (int k = 0; k < n; ++k)
+      p->pl.current_path.push_back(wp(xyzh[4 * k], xyzh[4 * k + 1], xyzh[4 * k + 2], xyzh[4 * k + 3]));
+    return DYMU_OK;
+  });
+}
+
+namespace {
+int put_path(const std::vector<base::Waypoint>& path, double* out, int max_wp) {
+  const int n = (int)path.size();
+  for (int k = 0; k < n && k < max_wp; ++k) {
+    out[4 * k + 0] = path[k].position[0];
+    out[4 * k + 1] = path[k].position[1];
+    out[4 * k + 2] = path[k].position[2];
+    out[4 * k + 3] = path[k].heading;
+  }
+  return n;
+}
+}  // namespace
+
+int dymu_planner_get_current_path(dymu_planner* p, double* out, int max_wp) {
+  if (!p || !out || max_wp < 0) return DYMU_ERR_ARG;
+  return put_path(p->pl.current_path, out, max_wp);
+}
+
+int dymu_planner_compute_local_planning(dymu_planner* p, double x, double y, double z, double h,
+                                        const uint8_t* image, uint32_t width, uint32_t height,
+                                        uint32_t row_size, uint32_t pixel_size, double res,
+                                        double* traj, int max_traj, int* n_traj,
+                                        double* local_time_s) {
+  if (!p || (!image && width && height) || max_traj < 0 || (max_traj > 0 && !traj) ||
+      (height > 0 && width > 0 && (uint64_t)(height - 1) * row_size + (uint64_t)(width - 1) * pixel_size >= (uint64_t)height * row_size))
+    return DYMU_ERR_ARG;
+  return guarded([&] {
+    base::samples::frame::Frame f;
+    f.width = width;
+    f.height = height;
+    f.row_size = row_size;
+    f.pixel_size = pixel_size;
+    f.image.assign(image, image + (size_t)height * row_size);
+    std::vector<base::Waypoint> trajectory;
+    base::Time t;
+    const bool r = p->pl.computeLocalPlanning(wp(x, y, z, h), f, res, trajectory, t);
+    if (r) {
+      const int n = put_path(trajectory, traj, max_traj);
+      if (n_traj) *n_traj = n;
+      if (local_time_s) *local_time_s = t.toSeconds();
+    } else if (n_traj) {
+      *n_traj = 0;
+    }
+    return (int)r;
+  });
+}
+
+int dymu_planner_repair_path(dymu_planner* p, double x, double y, double z, double h,
+                             uint32_t index) {
+  if (!p) return DYMU_ERR_ARG;
+  return guarded([&] { return p->pl.repairPath(wp(x, y, z, h), index); });
+}
+
+int dymu_planner_evaluate_path(dymu_planner* p, uint32_t starting_index) {
+  if (!p) return DYMU_ERR_ARG;
+  return guarded([&] { return (int)p->pl.evaluatePath(starting_index); });
+}
+
+int dymu_planner_expand_risk(dymu_planner* p) {
+  if (!p) return DYMU_ERR_ARG;
+  return guarded([&] { p->pl.expandRisk(); return DYMU_OK; });
+}
+
+int dymu_planner_compute_local_propagation(dymu_planner* p, const double* s, const double* o,
+                                           double* set_xy) {
+  if (!p || !s || !o) return DYMU_ERR_ARG;
+  return guarded([&] {
+    const auto n = p->pl.computeLocalPropagation(wp(s[0], s[1], s[2], s[3]), wp(o[0], o[1], o[2], o[3]));
+    if (!n) return 0;
+    if (set_xy) {
+      set_xy[0] = n->global_pose.position[0];
+      set_xy[1] = n->global_pose.position[1];
+    }
+    return 1;
+  });
+}
+
+int dymu_planner_get_risk_matrix(dymu_planner* p, double x, double y, double z, double h,
+                                 double* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  return guarded([&] { from_rows(p->pl.getRiskMatrix(wp(x, y, z, h)), out); return DYMU_OK; });
+}
+
+int dymu_planner_get_deviation_matrix(dymu_planner* p, double x, double y, double z, double h,
+                                      double* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  return guarded([&] { from_rows(p->pl.getDeviationMatrix(wp(x, y, z, h)), out); return DYMU_OK; });
+}
+
+int dymu_planner_get_reconnecting_index(dymu_planner* p) {
+  if (!p) return DYMU_ERR_ARG;
+  return p->pl.getReconnectingIndex();
+}
+
+int dymu_planner_res_ratio(dymu_planner* p) {
+  if (!p) return DYMU_ERR_ARG;
+  return (int)p->pl.resRatio();
+}
+
+int64_t dymu_planner_local_map_mask(dymu_planner* p, uint8_t* mask) {
+  if (!p) return DYMU_ERR_ARG;
+  return (int64_t)p->pl.localMapMask(mask);
+}
+
+int dymu_planner_local_block(dymu_planner* p, uint32_t i, uint32_t j, double* dev, double* tc,
+                             double* risk, uint8_t* state, uint8_t* obst) {
+  if (!p) return DYMU_ERR_ARG;
+  return (int)p->pl.localBlock(i, j, dev, tc, risk, state, obst);
+}
+
 }  // extern "C"

@@ -424,7 +424,34 @@ PLANNER_SYMBOLS = {
     "dymu_planner_set_hazard_density_window": (_i32, [_vp, _u32, _u32, _u32, _u32, _dp]),
     "dymu_planner_set_trafficability_window": (_i32, [_vp, _u32, _u32, _u32, _u32, _dp]),
     "dymu_planner_last_band_size": (ctypes.c_int64, [_vp]),
+    "dymu_planner_get_global_node": (_i32, [_vp, _u32, _u32, _vp]),
+    "dymu_planner_is_safe_node": (_i32, [_vp, _u32, _u32]),
+    "dymu_planner_is_fully_closed_node": (_i32, [_vp, _u32, _u32]),
+    "dymu_planner_reset_total_cost_map": (_i32, [_vp]),
+    "dymu_planner_load_total_cost_map": (_i32, [_vp, _dp]),
+    "dymu_planner_set_current_path": (_i32, [_vp, _vp, _i32]),
+    "dymu_planner_get_current_path": (_i32, [_vp, _dp, _i32]),
+    "dymu_planner_compute_local_planning": (_i32, [_vp, _d, _d, _d, _d, _vp, _u32, _u32, _u32,
+                                                   _u32, _d, _dp, _i32, ctypes.POINTER(_i32),
+                                                   ctypes.POINTER(_d)]),
+    "dymu_planner_repair_path": (_i32, [_vp, _d, _d, _d, _d, _u32]),
+    "dymu_planner_evaluate_path": (_i32, [_vp, _u32]),
+    "dymu_planner_expand_risk": (_i32, [_vp]),
+    "dymu_planner_compute_local_propagation": (_i32, [_vp, _dp, _dp, _dp]),
+    "dymu_planner_get_risk_matrix": (_i32, [_vp, _d, _d, _d, _d, _dp]),
+    "dymu_planner_get_deviation_matrix": (_i32, [_vp, _d, _d, _d, _d, _dp]),
+    "dymu_planner_get_reconnecting_index": (_i32, [_vp]),
+    "dymu_planner_res_ratio": (_i32, [_vp]),
+    "dymu_planner_local_map_mask": (ctypes.c_int64, [_vp, _vp]),
+    "dymu_planner_local_block": (_i32, [_vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp]),
 }
+
+
+class DymuGlobalNode(ctypes.Structure):
+    _fields_ = [("elevation", _d), ("slope", _d), ("raw_cost", _d), ("cost", _d),
+                ("hazard_density", _d), ("trafficability", _d), ("total_cost", _d),
+                ("terrain", _u32), ("state", _i32), ("is_obstacle", _i32),
+                ("has_local_map", _i32)]
 
 _pl = None
 
@@ -593,3 +620,111 @@ class Planner:
         st = DymuStats()
         _check(self._lib.dymu_planner_last_stats(self.h, ctypes.byref(st)))
         return st.as_dict()
+
+    # ---- node-level access (src/DyMu.hpp:500-518) ----
+    def getGlobalNode(self, i: int, j: int):
+        """Snapshot dict of node (i, j), or None (the reference's NULL)."""
+        n = DymuGlobalNode()
+        if not _b(self._lib.dymu_planner_get_global_node(self.h, i, j, ctypes.byref(n))):
+            return None
+        return {f: getattr(n, f) for f, _ in DymuGlobalNode._fields_}
+
+    def isSafeNode(self, i: int, j: int) -> bool:
+        return _b(self._lib.dymu_planner_is_safe_node(self.h, i, j))
+
+    def isFullyClosedNode(self, i: int, j: int) -> bool:
+        return _b(self._lib.dymu_planner_is_fully_closed_node(self.h, i, j))
+
+    def resetTotalCostMap(self):
+        _check(self._lib.dymu_planner_reset_total_cost_map(self.h))
+
+    def loadTotalCostMap(self, T) -> bool:
+        return _b(self._lib.dymu_planner_load_total_cost_map(self.h, self._grid(T)))
+
+    @property
+    def current_path(self) -> np.ndarray:
+        n = _b_int(self._lib.dymu_planner_get_current_path(self.h, np.empty(0), 0))
+        buf = np.empty(4 * max(n, 1))
+        self._lib.dymu_planner_get_current_path(self.h, buf, n)
+        return buf[:4 * n].reshape(-1, 4).copy()
+
+    @current_path.setter
+    def current_path(self, wps):
+        a = np.ascontiguousarray(np.asarray(wps, dtype=np.float64).reshape(-1, 4))
+        _check(self._lib.dymu_planner_set_current_path(self.h, a.ctypes.data, len(a)))
+
+    # ---- local layer (src/DyMu_LocalPathRepairing.cpp) ----
+    def computeLocalPlanning(self, w, image, res):
+        """image: uint8 [height, width] (nonzero = obstacle) or [height, width,
+        pixel_size].  Returns (repaired, trajectory [n, 4], local_time_s)."""
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, wd = img.shape[:2]
+        ps = img.shape[2] if img.ndim == 3 else 1
+        cap = max(64, 4 * len(self.current_path) + 4096)
+        buf = np.empty(4 * cap)
+        n = ctypes.c_int32()
+        t = ctypes.c_double()
+        r = _b(self._lib.dymu_planner_compute_local_planning(
+            self.h, *self._wp(w), img.ctypes.data, wd, h, wd * ps, ps, res, buf, cap,
+            ctypes.byref(n), ctypes.byref(t)))
+        if not r:
+            return False, np.empty((0, 4)), 0.0
+        if n.value > cap:
+            return True, self.current_path, t.value
+        return True, buf[:4 * n.value].reshape(-1, 4).copy(), t.value
+
+    def repairPath(self, w, index: int) -> int:
+        rc = self._lib.dymu_planner_repair_path(self.h, *self._wp(w), index)
+        if rc < -1:
+            raise DymuError(rc)
+        return rc
+
+    def evaluatePath(self, starting_index: int) -> bool:
+        return _b(self._lib.dymu_planner_evaluate_path(self.h, starting_index))
+
+    def expandRisk(self):
+        _check(self._lib.dymu_planner_expand_risk(self.h))
+
+    def computeLocalPropagation(self, w_init, w_overtake):
+        """The set node's global pose (x, y), or None."""
+        s = np.array(self._wp(w_init))
+        o = np.array(self._wp(w_overtake))
+        xy = np.empty(2)
+        if not _b(self._lib.dymu_planner_compute_local_propagation(self.h, s, o, xy)):
+            return None
+        return float(xy[0]), float(xy[1])
+
+    def resRatio(self) -> int:
+        return _b_int(self._lib.dymu_planner_res_ratio(self.h))
+
+    def _window(self, fn, w):
+        ls = 21 * self.resRatio()
+        out = np.empty((ls, ls))
+        _check(fn(self.h, *self._wp(w), out))
+        return out
+
+    def getRiskMatrix(self, w):
+        return self._window(self._lib.dymu_planner_get_risk_matrix, w)
+
+    def getDeviationMatrix(self, w):
+        return self._window(self._lib.dymu_planner_get_deviation_matrix, w)
+
+    def getReconnectingIndex(self) -> int:
+        return self._lib.dymu_planner_get_reconnecting_index(self.h)
+
+    def localMapMask(self):
+        m = np.zeros((self.ny, self.nx), dtype=np.uint8)
+        _b_int(self._lib.dymu_planner_local_map_mask(self.h, m.ctypes.data))
+        return m
+
+    def localBlock(self, i: int, j: int):
+        """(dev, tc, risk, state, obst) of node (i, j)'s r x r sub-cells, or None."""
+        r = self.resRatio()
+        dev, tc, risk = (np.empty((r, r)) for _ in range(3))
+        st, ob = (np.empty((r, r), dtype=np.uint8) for _ in range(2))
+        if not _b(self._lib.dymu_planner_local_block(self.h, i, j, dev.ctypes.data,
+                                                    tc.ctypes.data, risk.ctypes.data,
+                                                    st.ctypes.data, ob.ctypes.data)):
+            return None
+        return dev, tc, risk, st, ob
+

@@ -39,7 +39,125 @@ _SIGS = {
     "oracle_total_cost_matrix": (None, [_dp, _u64, _dp]),
     "oracle_global_path": (ctypes.c_int, [_dp, _vp, _u32, _u32, _d, _u32, _u32, _d, _d, _d, _d,
                                           _d, _dp, ctypes.c_int]),
+    "oracle_local_create": (_vp, [_u32, _u32, _d, _d, _d, _d, _d, _d, _d, ctypes.c_int]),
+    "oracle_local_destroy": (None, [_vp]),
+    "oracle_local_set_global": (None, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _d]),
+    "oracle_local_get_global": (None, [_vp, _vp, _vp]),
+    "oracle_local_set_path": (None, [_vp, _vp, ctypes.c_int]),
+    "oracle_local_get_path": (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
+    "oracle_local_reconnecting_index": (ctypes.c_int, [_vp]),
+    "oracle_local_planning": (ctypes.c_int, [_vp, _d, _d, _d, _d, _vp, _u32, _u32, _u32, _u32,
+                                             _d]),
+    "oracle_local_get_path_eval": (ctypes.c_int, [_vp, _d, _d, _d, _d, _vp, ctypes.c_int]),
+    "oracle_local_risk_matrix": (None, [_vp, _d, _d, _vp]),
+    "oracle_local_deviation_matrix": (None, [_vp, _d, _d, _vp]),
+    "oracle_local_map_mask": (_u64, [_vp, _vp]),
+    "oracle_local_block": (ctypes.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp]),
 }
+
+
+class OracleLocal:
+    """The local-layer restatement (oracle/oracle_local.c) over a copy of a
+    global layer: obstacle flags, total cost T (+inf unreachable), the CLOSED
+    state (default: finite T), elevation, hazard / trafficability, goal."""
+
+    def __init__(self, lib, nx, ny, gres, lres, offset=(0.0, 0.0), risk_distance=1.0,
+                 reconnect_distance=1.0, risk_ratio=1.0, approach=0):
+        self.lib = lib
+        self.nx, self.ny = nx, ny
+        self.r = int(gres / lres)
+        self.off = offset
+        self.h = lib.oracle_local_create(nx, ny, gres, lres, offset[0], offset[1], risk_distance,
+                                         reconnect_distance, risk_ratio, approach)
+
+    def close(self):
+        if self.h:
+            self.lib.oracle_local_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    @staticmethod
+    def _p(a, dt):
+        if a is None:
+            return None, None
+        a = np.ascontiguousarray(a, dtype=dt)
+        return a, a.ctypes.data
+
+    def set_global(self, obst, T, goal, goal_heading=0.0, closed=None, elev=None, hazard=None,
+                   traff=None):
+        if closed is None:
+            closed = np.isfinite(T)
+        keep = [self._p(obst, np.uint8), self._p(T, np.float64), self._p(closed, np.uint8),
+                self._p(elev, np.float64), self._p(hazard, np.float64),
+                self._p(traff, np.float64)]
+        self.lib.oracle_local_set_global(self.h, *[k[1] for k in keep], goal[0], goal[1],
+                                         goal_heading)
+
+    def hazard_traff(self):
+        hd = np.empty((self.ny, self.nx))
+        tr = np.empty((self.ny, self.nx))
+        self.lib.oracle_local_get_global(self.h, hd.ctypes.data, tr.ctypes.data)
+        return hd, tr
+
+    @property
+    def path(self):
+        n = self.lib.oracle_local_get_path(self.h, None, 0)
+        buf = np.empty(4 * max(n, 1))
+        self.lib.oracle_local_get_path(self.h, buf.ctypes.data, n)
+        return buf[:4 * n].reshape(-1, 4).copy()
+
+    @path.setter
+    def path(self, wps):
+        a = np.ascontiguousarray(np.asarray(wps, dtype=np.float64).reshape(-1, 4))
+        self.lib.oracle_local_set_path(self.h, a.ctypes.data, len(a))
+
+    def reconnecting_index(self):
+        return self.lib.oracle_local_reconnecting_index(self.h)
+
+    def local_planning(self, w, image, res):
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        h, wd = img.shape[:2]
+        ps = img.shape[2] if img.ndim == 3 else 1
+        w = tuple(w) + (0.0,) * (4 - len(w))
+        r = self.lib.oracle_local_planning(self.h, w[0], w[1], w[2], w[3], img.ctypes.data, wd, h,
+                                           wd * ps, ps, res)
+        return bool(r), (self.path if r else np.empty((0, 4)))
+
+    def get_path(self, w):
+        w = tuple(w) + (0.0,) * (4 - len(w))
+        n = self.lib.oracle_local_get_path_eval(self.h, w[0], w[1], w[2], w[3], None, 0)
+        p = self.path
+        p[:, 0] += self.off[0]
+        p[:, 1] += self.off[1]
+        return n, p
+
+    def _window(self, fn, x, y):
+        ls = 21 * self.r
+        out = np.empty((ls, ls))
+        fn(self.h, x, y, out.ctypes.data)
+        return out
+
+    def risk_matrix(self, x, y):
+        return self._window(self.lib.oracle_local_risk_matrix, x, y)
+
+    def deviation_matrix(self, x, y):
+        return self._window(self.lib.oracle_local_deviation_matrix, x, y)
+
+    def map_mask(self):
+        m = np.zeros((self.ny, self.nx), dtype=np.uint8)
+        self.lib.oracle_local_map_mask(self.h, m.ctypes.data)
+        return m
+
+    def block(self, i, j):
+        r = self.r
+        dev, tc, risk = (np.empty((r, r)) for _ in range(3))
+        st, ob = (np.empty((r, r), dtype=np.uint8) for _ in range(2))
+        if not self.lib.oracle_local_block(self.h, i, j, dev.ctypes.data, tc.ctypes.data,
+                                           risk.ctypes.data, st.ctypes.data, ob.ctypes.data):
+            return None
+        return dev, tc, risk, st, ob
 
 
 class Oracle:
@@ -167,6 +285,9 @@ class Oracle:
         if n < 0:
             return n, None
         return n, wp[:4 * n].reshape(n, 4).copy()
+
+    def local(self, nx, ny, gres, lres, **kw):
+        return OracleLocal(self.lib, nx, ny, gres, lres, **kw)
 
 
 _cached = None
