@@ -219,8 +219,9 @@ int dymu_resolve_window_device(dymu_ctx* ctx, const double* dF, double* dT, uint
                                uint32_t i0, uint32_t j0, uint32_t w, uint32_t h, void* stream,
                                dymu_stats* stats);
 /* The same with the caller's knowledge of the change: decrease_only != 0
- * promises that no speed in the window increased (a trafficability drop,
- * reference src/DyMu_LocalPathRepairing.cpp:389-394, or a cleared hazard).  Then
+ * promises that no F in the window increased (F grows with hazard density and
+ * falls with trafficability, reference :527-528: e.g. a hazard cleared or a
+ * trafficability restored after src/DyMu_LocalPathRepairing.cpp:389-394).  Then
  * the old map is a valid upper bound everywhere and no cell is reset: only the
  * window's tiles are seeded and the passes lower what the cheaper window
  * reaches.  decrease_only = 0 is dymu_resolve_window_device. */

@@ -243,10 +243,14 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
                              st));
     // default per pass: 64 8x8 tiles per CU (v4) / 8 16x16 tiles per CU (v5), the
     // measured optima at 8192^2..16384^2; 4 per CU for whole grids below 2^17 16x16
-    // tiles (4096^2: 6.28 vs 6.50 ms, v11)
-    const bool small5 = D.variant == 5 && !ghost_lo && !ghost_hi && ntiles < (1u << 17);
-    a.target = c->prio_target ? c->prio_target
-                              : (uint32_t)c->cu_count * (D.variant == 5 ? (small5 ? 4u : 8u) : 64u);
+    // tiles (4096^2: 6.28 vs 6.50 ms, v11) and 10 per CU for whole grids from 2^20
+    // (16384^2: 35.8 vs 36.9 ms, v18, profiles/r02/sweep_v18b.log)
+    const bool whole5 = D.variant == 5 && !ghost_lo && !ghost_hi;
+    const uint32_t per_cu = D.variant != 5 ? 64u
+                            : (whole5 && ntiles < (1u << 17)) ? 4u
+                            : (whole5 && ntiles >= (1u << 20)) ? 10u
+                                                               : 8u;
+    a.target = c->prio_target ? c->prio_target : (uint32_t)c->cu_count * per_cu;
     a.target_frac = c->prio_frac;
     a.prune = c->prune;
     a.delta = prio_delta(c);

@@ -205,6 +205,24 @@ __device__ __forceinline__ double two_sided_approx(double ty, double d, double c
   return __builtin_fma(s, t, __builtin_fma(d, 0.5, ty));
 }
 
+// two_sided_approx on two independent cells, statement by statement interleaved
+// (same operations, bit-identical)
+__device__ __forceinline__ void two_sided_approx2(double ty0, double d0, double c0, double ty1,
+                                                  double d1, double c1, double& v0, double& v1) {
+  const double r0 = __builtin_fma(-d0, d0, c0);
+  const double r1 = __builtin_fma(-d1, d1, c1);
+  const double y0 = __builtin_amdgcn_rsq(r0);
+  const double y1 = __builtin_amdgcn_rsq(r1);
+  const double h0 = __builtin_fma(d0, 0.5, ty0);
+  const double h1 = __builtin_fma(d1, 0.5, ty1);
+  const double s0 = r0 * y0;
+  const double s1 = r1 * y1;
+  const double t0 = __builtin_fma(-(y0 * 0.25), s0, 0.75);
+  const double t1 = __builtin_fma(-(y1 * 0.25), s1, 0.75);
+  v0 = __builtin_fma(s0, t0, h0);
+  v1 = __builtin_fma(s1, t1, h1);
+}
+
 // One cell of the reference update (:504-537) against the image.  Preconditions
 // (guaranteed by the skip test): f finite and min(Tx,Ty) finite, so the
 // reference's "Tx < inf && Ty < inf" is implied by |Tx - Ty| < C.
@@ -615,8 +633,7 @@ __device__ __forceinline__ void rb_update2(const double* p, const double* pn, co
     double v0, v1;  // two-sided candidates
     if constexpr (FAST && APPROX) {
       // an obstacle (f = inf) gives NaN here (rsq(inf) * inf), which v_min ignores
-      v0 = two_sided_approx(ty0, d0, c20);
-      v1 = two_sided_approx(ty1, d1, c21);
+      two_sided_approx2(ty0, d0, c20, ty1, d1, c21, v0, v1);
     } else {
       const double r0 = c20 - d0 * d0, r1 = c21 - d1 * d1;
       double q0, q1;
