@@ -12,7 +12,7 @@
  * insertion and erase order, and linear scans for every minimum / maximum.
  *
  * Where the reference has undefined behaviour this restatement defines it (the
- * product defines it the same way; DESIGN.md s6):
+ * product defines it the same way; DESIGN.md s4.7):
  *   U1 a NULL neighbour or node that the reference would dereference reads as
  *      absent: deviation/total cost +inf, elevation 0, the operation that needs
  *      it reports failure (GDM step -> degenerate; propagation -> NULL);

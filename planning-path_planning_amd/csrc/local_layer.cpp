@@ -10,7 +10,7 @@
 // and evaluation order (-ffp-contract=off), so results are bit-identical to
 // the oracle restatement (oracle/oracle_local.c, tests/test_local_layer.py).
 // Where the reference has undefined behaviour the definitions U1-U5 of
-// DESIGN.md s6 apply (the oracle defines them the same way).
+// DESIGN.md s4.7 apply (the oracle defines them the same way).
 #include <algorithm>
 #include <cmath>
 #include <limits>
@@ -23,11 +23,6 @@ namespace PathPlanning_lib {
 namespace {
 constexpr double kInf = std::numeric_limits<double>::infinity();
 constexpr int kMaxLocalSteps = 100000;  // U4
-
-// (uint) of a double as x86-64 GCC converts it (through int64)
-inline uint32_t to_u32(double d) {
-  return (d > -9.2e18 && d < 9.2e18) ? (uint32_t)(int64_t)d : 0u;
-}
 
 inline double eikonal(double tx, double ty, double C) {
   if ((std::fabs(tx - ty) < C) && (tx < kInf) && (ty < kInf))
@@ -75,7 +70,7 @@ inline CellPose cell_pose(const LocalLayer& L, uint64_t p, unsigned nx, double g
 
 // G:570-584 (index of the nearest global node, -1 = NULL)
 int64_t DyMuPathPlanner::nearestIndex(double x, double y) const {
-  const uint32_t i = to_u32(x / global_res_ + 0.5), j = to_u32(y / global_res_ + 0.5);
+  const uint32_t i = grid_u32(x / global_res_ + 0.5), j = grid_u32(y / global_res_ + 0.5);
   if (i >= nx_ || j >= ny_) return -1;
   return (int64_t)idx(i, j);
 }
@@ -104,7 +99,7 @@ int64_t DyMuPathPlanner::localAt(double x, double y) {
   const double cornerX = (double)gi - global_res_ / 2;
   const double cornerY = (double)gj - global_res_ / 2;
   const double a = x - cornerX, b = y - cornerY;
-  const uint32_t li = to_u32(a * L.r), lj = to_u32(b * L.r);
+  const uint32_t li = grid_u32(a * L.r), lj = grid_u32(b * L.r);
   if (li >= L.r || lj >= L.r) return -1;  // U2
   return (int64_t)((uint64_t)L.block(g) * L.rr + (uint64_t)lj * L.r + li);
 }
@@ -148,7 +143,7 @@ std::optional<localNode> DyMuPathPlanner::getLocalNode(base::Pose2D pos) {
 // :473-491 (bilinear in the parent's total costs; no CLOSED test)
 double DyMuPathPlanner::localTotalCost(uint64_t p) const {
   const CellPose c = cell_pose(*local_, p, nx_, global_res_);
-  const uint32_t i = to_u32(c.gx), j = to_u32(c.gy);
+  const uint32_t i = grid_u32(c.gx), j = grid_u32(c.gy);
   const double a = c.gx - (double)i, b = c.gy - (double)j;
   const int64_t n00 = nearestIndex(c.px, c.py);
   if (n00 < 0) return kInf;  // U1
@@ -402,7 +397,7 @@ bool DyMuPathPlanner::computeLocalWaypointGDM(base::Waypoint& wPos, double tau) 
   const LocalLayer& L = *local_;
   const double gx = wPos.position[0] - global_offset_[0];
   const double gy = wPos.position[1] - global_offset_[1];
-  const uint32_t cX = to_u32(gx / global_res_), cY = to_u32(gy / global_res_);
+  const uint32_t cX = grid_u32(gx / global_res_), cY = grid_u32(gy / global_res_);
   const double dX = gx - (double)cX, dY = gy - (double)cY;
   auto elev = [&](uint32_t i, uint32_t j) {  // U1: a NULL corner reads 0
     return (i < nx_ && j < ny_) ? elevation_[idx(i, j)] : 0.0;
@@ -625,10 +620,10 @@ bool DyMuPathPlanner::computeLocalPlanning(base::Waypoint wPos,
   wPos.position[0] -= global_offset_[0];
   wPos.position[1] -= global_offset_[1];
   const unsigned height = traversabilityMap.getHeight(), width = traversabilityMap.getWidth();
-  const uint32_t a = to_u32(std::fmax(0, ((wPos.position[1] - (double)height / 2 * res) / global_res_)));
-  const uint32_t b = to_u32(std::fmin((double)ny_, ((wPos.position[1] + (double)height / 2 * res) / global_res_)));
-  const uint32_t c = to_u32(std::fmax(0, ((wPos.position[0] - (double)width / 2 * res) / global_res_)));
-  const uint32_t d = to_u32(std::fmin((double)nx_, ((wPos.position[0] + (double)width / 2 * res) / global_res_)));
+  const uint32_t a = grid_u32(std::fmax(0, ((wPos.position[1] - (double)height / 2 * res) / global_res_)));
+  const uint32_t b = grid_u32(std::fmin((double)ny_, ((wPos.position[1] + (double)height / 2 * res) / global_res_)));
+  const uint32_t c = grid_u32(std::fmax(0, ((wPos.position[0] - (double)width / 2 * res) / global_res_)));
+  const uint32_t d = grid_u32(std::fmin((double)nx_, ((wPos.position[0] + (double)width / 2 * res) / global_res_)));
   for (uint32_t j = a; j < b; ++j)
     for (uint32_t i = c; i < d; ++i) subdivideGlobalNode(i, j);
   unsigned minIndex = (unsigned)current_path.size(), maxIndex = 0;

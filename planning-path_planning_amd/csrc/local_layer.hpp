@@ -20,6 +20,14 @@
 
 namespace PathPlanning_lib {
 
+// (uint) of a double as the reference's x86-64 GCC build converts it: through
+// int64 (cvttsd2si), so -1 < d < 0 gives 0 and more negative values wrap to
+// huge indices that every bounds test rejects.  A plain cast of a negative
+// double to unsigned is undefined behaviour in C++.
+inline uint32_t grid_u32(double d) {
+  return (d > -9.2e18 && d < 9.2e18) ? (uint32_t)(int64_t)d : 0u;
+}
+
 struct LocalLayer {
   unsigned r = 1;   // res_ratio
   uint64_t rr = 1;  // r * r

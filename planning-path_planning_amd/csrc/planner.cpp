@@ -74,7 +74,7 @@ bool DyMuPathPlanner::initGlobalLayer(double globalres, double localres, unsigne
   local_res_ = localres;
   {
     const double rr = global_res_ / local_res_;  // :49 res_ratio = (uint)(global_res / local_res)
-    res_ratio_ = (rr > -9.2e18 && rr < 9.2e18) ? (unsigned)(int64_t)rr : 0u;
+    res_ratio_ = grid_u32(rr);
   }
   if (!local_) local_ = std::make_unique<LocalLayer>();
   local_->reset(res_ratio_);
@@ -244,7 +244,7 @@ bool DyMuPathPlanner::setGoal(base::Waypoint wGoal) {
   const double px = (wGoal.position[0] - global_offset_[0]) / global_res_;
   const double py = (wGoal.position[1] - global_offset_[1]) / global_res_;
   if (px < 0 || py < 0) return false;
-  const unsigned i = (unsigned)(px + 0.5), j = (unsigned)(py + 0.5);
+  const unsigned i = grid_u32(px + 0.5), j = grid_u32(py + 0.5);
   if (i >= nx_ || j >= ny_) return false;
   if (i == 0 || j == 0 || i + 1 >= nx_ || j + 1 >= ny_) return false;  // an nb4 is NULL
   const uint64_t k = idx(i, j);
@@ -640,7 +640,7 @@ bool DyMuPathPlanner::computeTotalCostMap(base::Waypoint wPos) {
     log_error("PLANNER: The rover is located too close to an obstacle");
     return false;
   }
-  const unsigned si = (unsigned)fx, sj = (unsigned)fy;
+  const unsigned si = grid_u32(fx), sj = grid_u32(fy);
   if (!safeNode(si, sj)) {
     log_error("PLANNER: The rover is located too close to an obstacle");
     return false;
@@ -707,7 +707,7 @@ bool DyMuPathPlanner::computeGlobalPath(base::Waypoint wPos) {
 base::Waypoint DyMuPathPlanner::computeNextGlobalWaypoint(base::Waypoint& wPos, double tau) {
   base::Waypoint wNext;
   const double gx = wPos.position[0] / global_res_, gy = wPos.position[1] / global_res_;
-  const unsigned cx = (unsigned)gx, cy = (unsigned)gy;
+  const unsigned cx = grid_u32(gx), cy = grid_u32(gy);
   const double ax = gx - (double)cx, ay = gy - (double)cy;
   if (cx + 1 >= nx_ || cy + 1 >= ny_) {  // reference: NULL dereference
     wNext.position[0] = wNext.position[1] = std::numeric_limits<double>::quiet_NaN();
@@ -765,7 +765,7 @@ double DyMuPathPlanner::interpolate(double a, double b, double g00, double g01, 
 std::string DyMuPathPlanner::getLocomotionMode(base::Waypoint wPos) {
   const double x = wPos.position[0] - global_offset_[0];
   const double y = wPos.position[1] - global_offset_[1];
-  const unsigned i = (unsigned)(x / global_res_ + 0.5), j = (unsigned)(y / global_res_ + 0.5);
+  const unsigned i = grid_u32(x / global_res_ + 0.5), j = grid_u32(y / global_res_ + 0.5);
   if (i >= nx_ || j >= ny_) return "DONT_CARE";
   const int m = loc_mode_[idx(i, j)];
   if (m < 0 || m >= (int)locomotion_modes_.size()) return "DONT_CARE";
@@ -815,17 +815,17 @@ std::vector<std::vector<double>> DyMuPathPlanner::getTrafficabilityMatrix() {
 double DyMuPathPlanner::getTotalCost(base::Waypoint wInt) {
   const double x = wInt.position[0] - global_offset_[0];
   const double y = wInt.position[1] - global_offset_[1];
-  const unsigned i = (unsigned)(x / global_res_), j = (unsigned)(y / global_res_);
+  const unsigned i = grid_u32(x / global_res_), j = grid_u32(y / global_res_);
   const double a = x - (double)i, b = y - (double)j;
   if (i >= nx_ || j >= ny_ || i + 1 >= nx_ || j + 1 >= ny_) {  // a corner is NULL
-    const unsigned ni = (unsigned)(x / global_res_ + 0.5), nj = (unsigned)(y / global_res_ + 0.5);
+    const unsigned ni = grid_u32(x / global_res_ + 0.5), nj = grid_u32(y / global_res_ + 0.5);
     if (ni >= nx_ || nj >= ny_) return kInf;
     return T(idx(ni, nj));
   }
   const uint64_t k = idx(i, j);
   const uint64_t k10 = k + 1, k01 = k + nx_, k11 = k + nx_ + 1;
   if (!closedCell(k) || !closedCell(k10) || !closedCell(k01) || !closedCell(k11)) {
-    const unsigned ni = (unsigned)(x / global_res_ + 0.5), nj = (unsigned)(y / global_res_ + 0.5);
+    const unsigned ni = grid_u32(x / global_res_ + 0.5), nj = grid_u32(y / global_res_ + 0.5);
     return T(idx(ni, nj));
   }
   const double w00 = T(k), w10 = T(k10);

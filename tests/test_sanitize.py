@@ -1,0 +1,41 @@
+"""AddressSanitizer + UndefinedBehaviorSanitizer build of the host code
+(SURVEY s5): the planner (planner.cpp, local_layer.cpp, planner_capi.cpp) and
+the oracle restatements (oracle.c, oracle_local.c), driven by
+tests/sanitize/driver.cpp through the cost map, goal, path, the whole local
+layer and the flat C-ABI, checked against the oracle.  The HIP engine is
+replaced by tests/sanitize/engine_stub.c (every engine call returns
+DYMU_ERR_NO_DEVICE, as on a machine without a GPU), so no GPU runtime enters
+the sanitized process."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FLAGS = ["-g", "-O1", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+         "-fno-omit-frame-pointer", "-ffp-contract=off"]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs gcc/g++")
+def test_host_code_under_asan_ubsan(tmp_path):
+    inc = ["-I" + os.path.join(ROOT, d) for d in ("include", "oracle",
+                                                 "planning-path_planning_amd/csrc")]
+    objs = []
+    for src in ("oracle/oracle.c", "oracle/oracle_local.c", "tests/sanitize/engine_stub.c"):
+        o = str(tmp_path / (os.path.basename(src) + ".o"))
+        subprocess.run(["gcc", *FLAGS, "-std=gnu11", *inc, "-c", os.path.join(ROOT, src), "-o", o],
+                       check=True)
+        objs.append(o)
+    exe = str(tmp_path / "driver")
+    srcs = [os.path.join(ROOT, s) for s in (
+        "tests/sanitize/driver.cpp", "planning-path_planning_amd/csrc/planner.cpp",
+        "planning-path_planning_amd/csrc/local_layer.cpp",
+        "planning-path_planning_amd/csrc/planner_capi.cpp")]
+    subprocess.run(["g++", *FLAGS, "-std=c++17", *inc, *srcs, *objs, "-o", exe], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "sanitize driver ok" in r.stdout
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
