@@ -82,7 +82,8 @@ struct localNode {
   uint64_t id = 0;
 };
 
-struct LocalLayer;  // csrc/local_layer.cpp
+struct LocalLayer;  // csrc/local_layer.hpp
+struct PathIndex;   // csrc/local_layer.hpp
 
 class DyMuPathPlanner {
  public:
@@ -216,7 +217,8 @@ class DyMuPathPlanner {
   uint64_t localCell(uint64_t p, localNode* out) const;
   int64_t localAt(double x, double y);  // getLocalNode by sub-cell id, -1 = NULL
   double localTotalCost(uint64_t p) const;
-  bool isBlockingObstacle(uint64_t p, unsigned& maxIndex, unsigned& minIndex) const;
+  bool isBlockingObstacle(uint64_t p, unsigned& maxIndex, unsigned& minIndex,
+                          const PathIndex* index = nullptr) const;
   int64_t localPropagation(base::Waypoint wInit, base::Waypoint wOvertake);
   std::vector<base::Waypoint> localPath(uint64_t set, base::Waypoint wInit);
   void windowMatrix(base::Waypoint rover_pos, bool deviation, std::vector<std::vector<double>>& m);

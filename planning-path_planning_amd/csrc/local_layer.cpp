@@ -161,13 +161,38 @@ double DyMuPathPlanner::getTotalCost(const localNode& lNode) {
   return localTotalCost(lNode.id);
 }
 
-// :441-471
-bool DyMuPathPlanner::isBlockingObstacle(uint64_t p, unsigned& maxIndex, unsigned& minIndex) const {
+// :441-471.  With an index (computeLocalPlanning's pixel loop), the scan starts
+// at the first waypoint within risk_distance, found among the index's 3x3
+// cells; the reference's loop changes nothing before it.
+bool DyMuPathPlanner::isBlockingObstacle(uint64_t p, unsigned& maxIndex, unsigned& minIndex,
+                                         const PathIndex* index) const {
   const CellPose c = cell_pose(*local_, p, nx_, global_res_);
-  bool blocked = false;
-  for (unsigned i = 0; i < current_path.size(); ++i) {
+  auto near = [&](unsigned i) {
     const double dx = c.wx - current_path[i].position[0], dy = c.wy - current_path[i].position[1];
-    if (std::sqrt(dx * dx + dy * dy) < risk_distance_) {
+    return std::sqrt(dx * dx + dy * dy) < risk_distance_;
+  };
+  unsigned first = 0;
+  if (index) {
+    const int64_t cx = PathIndex::cell(c.wx, index->cs), cy = PathIndex::cell(c.wy, index->cs);
+    uint64_t best = UINT64_MAX;
+    for (int64_t a = cx - 1; a <= cx + 1; ++a)
+      for (int64_t b = cy - 1; b <= cy + 1; ++b) {
+        const auto it = index->cells.find(PathIndex::key(a, b));
+        if (it == index->cells.end()) continue;
+        for (const uint32_t k : it->second) {
+          if (k >= best) break;
+          if (near(k)) {
+            best = k;
+            break;
+          }
+        }
+      }
+    if (best == UINT64_MAX) return false;
+    first = (unsigned)best;
+  }
+  bool blocked = false;
+  for (unsigned i = first; i < current_path.size(); ++i) {
+    if (near(i)) {
       if (!blocked) {
         blocked = true;
         minIndex = (i < minIndex) ? i : minIndex;
@@ -633,6 +658,8 @@ bool DyMuPathPlanner::computeLocalPlanning(base::Waypoint wPos,
   const double gsx = global_res_ * (double)nx_ - 0.5, gsy = global_res_ * (double)ny_ - 0.5;
   const double r2 = (double)(res_ratio_ * res_ratio_);
   const uint32_t row = traversabilityMap.getRowSize(), pix = traversabilityMap.getPixelSize();
+  PathIndex index;
+  bool indexed = false, index_built = false;
   for (uint32_t j = 0; j < height; ++j)
     for (uint32_t i = 0; i < width; ++i) {
       const double px = offsetX + i * res, py = offsetY - j * res;
@@ -648,7 +675,12 @@ bool DyMuPathPlanner::computeLocalPlanning(base::Waypoint wPos,
         L.obst[l] = 1;
         L.expandable.push_back((uint64_t)l);
         L.risk[l] = 1.0;
-        const bool blocked = isBlockingObstacle((uint64_t)l, maxIndex, minIndex);
+        if (!index_built) {  // current_path does not change inside this loop
+          indexed = index.build(current_path, risk_distance_);
+          index_built = true;
+        }
+        const bool blocked =
+            isBlockingObstacle((uint64_t)l, maxIndex, minIndex, indexed ? &index : nullptr);
         pathBlocked = pathBlocked ? true : blocked;
         // :264-274 hazard feedback on the global layer (re-propagated by the
         // next computeTotalCostMap as a windowed update)

@@ -13,10 +13,13 @@
 // order instead of being stored.
 #pragma once
 
+#include <cmath>
 #include <cstdint>
 #include <deque>
 #include <unordered_map>
 #include <vector>
+
+#include "dymu_base.hpp"
 
 namespace PathPlanning_lib {
 
@@ -27,6 +30,34 @@ namespace PathPlanning_lib {
 inline uint32_t grid_u32(double d) {
   return (d > -9.2e18 && d < 9.2e18) ? (uint32_t)(int64_t)d : 0u;
 }
+
+// Waypoints of current_path bucketed on a square grid of cell size 1.5 x
+// risk_distance, for isBlockingObstacle (:441-471).  The reference scans the
+// whole path for every obstacle pixel; the first waypoint within risk_distance
+// of a point can only lie in the 3x3 cells around it (any pair closer than
+// risk_distance is less than 2/3 of a cell apart on each axis), and the
+// reference's scan changes nothing before that waypoint -- so the index gives
+// the same result from a handful of candidates.
+struct PathIndex {
+  double cs = 0.0;
+  std::unordered_map<uint64_t, std::vector<uint32_t>> cells;  // ascending indices
+  static int64_t cell(double v, double cs) { return (int64_t)std::floor(v / cs); }
+  static uint64_t key(int64_t cx, int64_t cy) {
+    return ((uint64_t)(uint32_t)(int32_t)cx << 32) | (uint64_t)(uint32_t)(int32_t)cy;
+  }
+  // false when the index cannot be used (the caller scans the path instead)
+  bool build(const std::vector<base::Waypoint>& path, double rd) {
+    cells.clear();
+    if (!(rd > 0) || !(rd < 1e300)) return false;
+    cs = 1.5 * rd;
+    for (uint32_t k = 0; k < path.size(); ++k) {
+      const double x = path[k].position[0], y = path[k].position[1];
+      if (!(std::fabs(x / cs) < 1e9) || !(std::fabs(y / cs) < 1e9)) return false;  // NaN / far
+      cells[key(cell(x, cs), cell(y, cs))].push_back(k);
+    }
+    return true;
+  }
+};
 
 struct LocalLayer {
   unsigned r = 1;   // res_ratio

@@ -210,3 +210,30 @@ def test_local_golden_terrain(dymu, oracle, name, approach):
     assert same(p.getTrafficabilityMatrix(), gold["traff"])
     assert same(p.getRiskMatrix(rover), gold["risk"])
     assert same(p.getDeviationMatrix(rover), gold["dev"])
+
+
+@pytest.mark.parametrize("approach", [0, 1])
+def test_blocking_on_self_crossing_path(dymu, oracle, approach):
+    """isBlockingObstacle (:441-471) takes the FIRST waypoint within
+    risk_distance and the run of blocked waypoints after it: a current_path
+    that loops back past the obstacle twice (the product finds that waypoint
+    through a spatial index of the path, the oracle by the reference's scan)."""
+    N = 48
+    p, o = build(dymu, oracle, N, 0.25, approach, goal=(40, 40))
+    t = np.linspace(0, 4 * np.pi, 160)
+    loop = np.stack([20 + 8 * np.cos(t + np.pi) + 0.05 * t, 20 + 8 * np.sin(t + np.pi) + 0.05 * t,
+                     np.zeros_like(t), np.zeros_like(t)], axis=1)
+    path = np.concatenate([loop, np.stack([np.linspace(loop[-1, 0], 39, 60),
+                                           np.linspace(loop[-1, 1], 39, 60),
+                                           np.zeros(60), np.zeros(60)], axis=1)])
+    p.current_path = path
+    o.path = path
+    rover = tuple(path[0, :2])
+    centre = (28.3, 20.6)  # on the loop, passed twice
+    img = disc_image(rover, centre, 0.9, 0.25, 160)
+    rep, traj, _ = p.computeLocalPlanning(rover, img, 0.25)
+    rep_o, traj_o = o.local_planning(rover, img, 0.25)
+    assert rep and rep == rep_o
+    assert len(traj) > 20
+    assert same(traj, traj_o)
+    compare_state(p, o, rover)
