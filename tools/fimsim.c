@@ -183,6 +183,48 @@ static int solve_tile(int tx, int ty, int method, int maxs, int* sweeps_out, uns
       memcpy(act, nact, nbx * nby);
       changed = 0;
       for (int q = 0; q < nbx * nby; q++) if (act[q]) changed = 1;
+    } else if (method == 8 || method == 9) {
+      // lockstep segments: every lane owns a 4-cell segment (method 8: rows in
+      // even sweeps, columns in odd ones; method 9: rows only) and all lanes
+      // update their k-th cell at step k from the current image (so the other
+      // segments' cells are as of their own step), direction alternating every
+      // two sweeps
+      static double* buf = 0;
+      if (!buf) buf = malloc(sizeof(double) * W * H);
+      const int orient = method == 9 ? 0 : (s & 1), dir = method == 9 ? (s & 1) : ((s >> 1) & 1);
+      for (int k = 0; k < 4; k++) {
+        const int kk = dir ? 3 - k : k;
+        int nb = 0;
+        if (orient == 0) {
+          for (int r = 1; r <= H; r++)
+            for (int sg = 0; sg < W / 4; sg++) {
+              const int c = sg * 4 + kk + 1;
+              buf[nb++] = eik(fmin(L[LI(r, c - 1)], L[LI(r, c + 1)]), fmin(L[LI(r - 1, c)], L[LI(r + 1, c)]), f[(r - 1) * W + (c - 1)]);
+            }
+          nb = 0;
+          for (int r = 1; r <= H; r++)
+            for (int sg = 0; sg < W / 4; sg++) {
+              const int c = sg * 4 + kk + 1;
+              cell_updates++;
+              if (buf[nb] < L[LI(r, c)]) { L[LI(r, c)] = buf[nb]; changed = 1; }
+              nb++;
+            }
+        } else {
+          for (int c = 1; c <= W; c++)
+            for (int sg = 0; sg < H / 4; sg++) {
+              const int r = sg * 4 + kk + 1;
+              buf[nb++] = eik(fmin(L[LI(r, c - 1)], L[LI(r, c + 1)]), fmin(L[LI(r - 1, c)], L[LI(r + 1, c)]), f[(r - 1) * W + (c - 1)]);
+            }
+          nb = 0;
+          for (int c = 1; c <= W; c++)
+            for (int sg = 0; sg < H / 4; sg++) {
+              const int r = sg * 4 + kk + 1;
+              cell_updates++;
+              if (buf[nb] < L[LI(r, c)]) { L[LI(r, c)] = buf[nb]; changed = 1; }
+              nb++;
+            }
+        }
+      }
     } else if (method == 7) {  // red-black (checkerboard) GS: red half-sweep then black
       for (int color = 0; color < 2; color++)
         for (int r = 1; r <= H; r++)
