@@ -159,6 +159,13 @@ KERNEL_NAMES = {3: "k_fim_pass_rb", 4: "k_fim_pass_prio<8>",
                 5: f"k_fim_pass_dyn<16, {'false' if _EXACT else 'true'}>"}
 
 
+def geometric_bound(N, gi, gj, tw, th):
+    """Largest Manhattan distance, in tiles, from the goal's tile to any tile."""
+    nt_x, nt_y = (N + tw - 1) // tw, (N + th - 1) // th
+    gx, gy = gi // tw, gj // th
+    return max(gx, nt_x - 1 - gx) + max(gy, nt_y - 1 - gy)
+
+
 def run_single(args):
     import dymu
 
@@ -172,7 +179,7 @@ def run_single(args):
         eng.solve_device(dF, dT, N, N, N, g[0], g[1])
     prof = not args.no_profile
     eng.set_profiling(PROFILE_PERIOD if prof else 0)
-    tot = {"passes": 0, "tile_visits": 0, "inner_sweeps": 0, "launches": 0}
+    tot = {"passes": 0, "tile_visits": 0, "inner_sweeps": 0, "launches": 0, "deferred": 0}
     kern_ms, kern_n = 0.0, 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -352,7 +359,13 @@ def main():
                                else f"{args.backend}, torch.distributed loop") + ")"),
             "exchange_rounds_per_solve": tot.get("rounds", 0) / K,
             "passes_per_solve": tot["passes"] / K,
+            # a tile is first relaxed one pass after its 4-neighbour that reaches it,
+            # so no solve takes fewer passes than the largest Manhattan tile distance
+            # from the goal's tile (1024 at 16384^2 with 16x16 tiles)
+            "passes_geometric_bound": geometric_bound(N, N // 2, N // 2, st.get("tile_w", 16),
+                                                      st.get("tile_h", 16)),
             "tile_visits_per_solve": tot["tile_visits"] / K,
+            "entries_deferred_per_solve": tot.get("deferred", 0) / K,
             "inner_sweeps_per_solve": tot["inner_sweeps"] / K,
             "pass_kernel": st.get("kernel"),
             "ranks_seen": tot.get("ranks_seen", 1),

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DYMU_ABI_VERSION 3
+#define DYMU_ABI_VERSION 4
 
 typedef enum dymu_status {
   DYMU_OK = 0,
@@ -79,6 +79,8 @@ typedef struct dymu_stats {
   int tile_w, tile_h;    /* tile geometry used */
   int kernel;            /* pass kernel that ran (see dymu_opts.kernel) */
   int reserved;
+  uint64_t deferred;     /* kernel 5: list entries deferred to a later pass (key above the
+                            pass's threshold bin); entries drawn = tile_visits + deferred */
 } dymu_stats;
 
 /* Context: owns a HIP stream, events and workspace on one device. */

@@ -467,6 +467,7 @@ int dom_finish(dymu_ctx* c, hipStream_t st, dymu_stats* stats, double ms) {
     stats->tile_visits = h[kStatVisits];
     stats->inner_sweeps = h[kStatSweeps];
     stats->max_active = h[kStatMaxActive];
+    stats->deferred = h[kStatDeferred];
     stats->rounds = 0;
     stats->ms = ms;
     stats->tile_w = tile_w(D.variant);

@@ -14,6 +14,7 @@ enum StatSlot : int {
   kStatVisits = 1,
   kStatSweeps = 2,
   kStatMaxActive = 3,
+  kStatDeferred = 4,
   kStatSlots = 8
 };
 

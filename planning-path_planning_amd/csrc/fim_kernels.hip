@@ -1065,7 +1065,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   __shared__ uint32_t s_hout[kBins];
   __shared__ uint32_t s_nq, s_base, s_next;
   __shared__ int s_bstar;
-  __shared__ unsigned long long s_visits, s_sweeps, s_minout;
+  __shared__ unsigned long long s_visits, s_sweeps, s_minout, s_defer;
   __shared__ unsigned long long s_ek[WPB][4];
   __shared__ double s_img[WPB][IMG];
 
@@ -1107,6 +1107,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       s_next = 0;
       s_visits = 0;
       s_sweeps = 0;
+      s_defer = 0;
       s_minout = kInfBits;
     }
   }
@@ -1143,7 +1144,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     }
   };
 
-  unsigned long long my_visits = 0, my_sweeps = 0;
+  unsigned long long my_visits = 0, my_sweeps = 0, my_defer = 0;
   double* img = s_img[wv];
   unsigned long long* ek = s_ek[wv];
   const uint32_t chunk = (n_active + gridDim.x - 1) / gridDim.x;
@@ -1170,6 +1171,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     if (lane == 0) a.key_in[tile] = kInfBits;
     if (sweeps < 0) {  // deferred to the next pass with its key
       if (lane == 0) enqueue(tile, kb);
+      ++my_defer;
       continue;
     }
     if (trace && tid == 0 && first) {
@@ -1204,19 +1206,21 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     first = false;
   }
   if (trace && tid == 0) trace[3] = __builtin_amdgcn_s_memrealtime();
-  if (lane == 0 && my_visits) {
+  if (lane == 0 && (my_visits || my_defer)) {
     atomicAdd(&s_visits, my_visits);
     atomicAdd(&s_sweeps, my_sweeps);
+    atomicAdd(&s_defer, my_defer);
   }
   __syncthreads();
   const uint32_t nq = s_nq < QCAP ? s_nq : QCAP;
   if (tid == 0) {
     if (nq) s_base = atomicAdd(&a.count_out[shard], nq);
     if (s_minout != kInfBits) atomicMin(a.minkey_out, s_minout);
-    if (s_visits) {
+    if (s_visits || s_defer) {
       unsigned long long* st = a.stats + (uint64_t)shard * kStatSlots;
       atomicAdd(&st[kStatVisits], s_visits);
       atomicAdd(&st[kStatSweeps], s_sweeps);
+      if (s_defer) atomicAdd(&st[kStatDeferred], s_defer);
     }
   }
   if (tid < kBins && s_hout[tid]) atomicAdd(&a.hist_out[shard * kBins + tid], s_hout[tid]);

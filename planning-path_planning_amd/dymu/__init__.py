@@ -87,6 +87,7 @@ class DymuStats(ctypes.Structure):
         ("tile_h", ctypes.c_int),
         ("kernel", ctypes.c_int),
         ("reserved", ctypes.c_int),
+        ("deferred", ctypes.c_uint64),
     ]
 
     def as_dict(self) -> dict:

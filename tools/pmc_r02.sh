@@ -1,0 +1,12 @@
+#!/bin/bash
+# PMC round on the current kernel: the 8-B/lane counter calibration
+# (tools/pmc_calib: known bytes) and the counter passes of tools/pmc_round.sh,
+# each pass a separate rocprofv3 --pmc run (no trace domains mixed in).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT="$R/gpurun_out/pmc"
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/c1" -o run -- "$R/tools/pmc_calib" 16384 > "$OUT/c1.log" 2>&1 || exit 1
+timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/c2" -o run -- "$R/tools/pmc_calib" 16384 > "$OUT/c2.log" 2>&1 || exit 1
+bash "$R/tools/pmc_round.sh"

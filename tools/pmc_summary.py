@@ -2,9 +2,11 @@
 HBM traffic of the dominant kernel for bench.py's roofline.traffic).
 
 FETCH_SIZE / WRITE_SIZE are in KiB.  MI355X_MICROARCH.md (HBM): FETCH_SIZE
-reports 1/2 of the bytes of wide coalesced streaming reads on gfx950, so it is
-doubled here; other access widths are uncalibrated there (our loads are 8 B
-per lane), which is why the raw value is kept beside the corrected one."""
+reports 1/2 of the bytes of wide coalesced streaming reads on gfx950 and other
+access widths are uncalibrated, so when the calibration passes of
+tools/pmc_r02.sh exist (c1: FETCH_SIZE, c2: WRITE_SIZE of tools/pmc_calib, which
+reads / writes a known 8 N^2 bytes with kernel 5's 8-B-per-lane tile pattern)
+the factors are measured from them; otherwise FETCH x2, WRITE x1."""
 import csv, glob, json, sys, collections
 root, tag = sys.argv[1], sys.argv[2]
 kern = sys.argv[3] if len(sys.argv) > 3 else "k_fim_pass"
@@ -19,12 +21,33 @@ for f in sorted(glob.glob(root + "/p*/run_counter_collection.csv")):
 n = len(disp["FETCH_SIZE"])
 fetch = tot["FETCH_SIZE"] * 1024.0
 write = tot["WRITE_SIZE"] * 1024.0
+ff, wf, calib = 2.0, 1.0, "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); 8-B/lane loads uncalibrated"
+
+
+def calib_total(path, kname, counter):
+    t = 0.0
+    for r in csv.DictReader(open(path)):
+        if kname in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            t += float(r["Counter_Value"])
+    return t * 1024.0
+
+
+c1 = glob.glob(root + "/c1/run_counter_collection.csv")
+c2 = glob.glob(root + "/c2/run_counter_collection.csv")
+if c1 and c2:
+    known = 8.0 * 16384 ** 2
+    ff = known / calib_total(c1[0], "k_read", "FETCH_SIZE")
+    wf = known / calib_total(c2[0], "k_write", "WRITE_SIZE")
+    calib = (f"measured on tools/pmc_calib (8-B/lane tile pattern, 2 GiB known): "
+             f"FETCH_SIZE x{ff:.4f}, WRITE_SIZE x{wf:.4f}")
 out = {
     "kernel": name, "dispatches": n, "grid": int(sys.argv[4]) if len(sys.argv) > 4 else 16384,
     "fetch_bytes_raw": fetch, "write_bytes": write,
-    "traffic_bytes_per_launch": (2.0 * fetch + write) / max(n, 1),
+    "traffic_bytes_per_launch": (ff * fetch + wf * write) / max(n, 1),
     "traffic_bytes_per_launch_raw": (fetch + write) / max(n, 1),
-    "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); 8-B/lane loads uncalibrated",
+    "fetch_bytes_per_launch": ff * fetch / max(n, 1),
+    "write_bytes_per_launch": wf * write / max(n, 1),
+    "correction": calib,
     "counters": {k: v for k, v in tot.items()},
 }
 json.dump(out, open(f"profiles/pmc_{tag}.json", "w"), indent=1)
