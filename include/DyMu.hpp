@@ -107,6 +107,11 @@ class DyMuPathPlanner {
                       std::vector<std::vector<double>> elevation,
                       std::vector<std::vector<double>> terrainMap);
 
+  // the per-node steps of computeCostMap (src/DyMu.hpp:493-497), by grid index
+  void calculateSlope(unsigned i, unsigned j);
+  void calculateNominalCost(unsigned i, unsigned j, int range, int numLocs);
+  void smoothCost(unsigned i, unsigned j);
+
   bool setGoal(base::Waypoint wGoal);
   bool computeTotalCostMap(base::Waypoint wPos);
   bool computeEntireTotalCostMap();
@@ -212,6 +217,7 @@ class DyMuPathPlanner {
   void gradientNode(unsigned i, unsigned j, double& dnx, double& dny) const;
   bool safeNode(unsigned i, unsigned j) const;
   std::optional<globalNode> snapshot(uint64_t k);
+  void nominalCost(unsigned i, unsigned j, int range, int num_locs, double cmax);
   // local layer internals (csrc/local_layer.cpp)
   int64_t nearestIndex(double x, double y) const;
   uint64_t localCell(uint64_t p, localNode* out) const;

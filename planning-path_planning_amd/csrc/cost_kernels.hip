@@ -69,7 +69,7 @@ __global__ void k_cost_nominal(CostArgs a) {
       obst = true;
     } else if ((uint64_t)(t + 1) * a.n_slopes * a.n_locs > (uint64_t)a.lut_len) {
       // terrain class beyond the LUT: the reference reads out of bounds (UB);
-      // here the cell becomes an obstacle (DESIGN.md s8)
+      // here the cell becomes an obstacle (DESIGN.md s4.6)
       raw = a.cmax;
       obst = true;
     } else if (a.n_slopes == 1) {  // :235-244, Q4: terrain*numLocs + i

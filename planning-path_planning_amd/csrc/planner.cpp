@@ -161,82 +161,112 @@ bool DyMuPathPlanner::computeCostMap(std::vector<double> cost_data,
                         : (uint32_t)terrainMap[j][i];
     }
   }
-  for (unsigned j = 0; j < ny_; ++j) {
+  for (unsigned j = 0; j < ny_; ++j)
     for (unsigned i = 0; i < nx_; ++i) {
+      calculateSlope(i, j);
+      nominalCost(i, j, range, num_locs, cmax);
       const uint64_t k = idx(i, j);
-      // calculateSlope (:186-210)
-      double dx, dy;
-      if (i == 0)
-        dx = (elevation_[k + 1] - elevation_[k]) / global_res_;
-      else if (i == nx_ - 1)
-        dx = (elevation_[k] - elevation_[k - 1]) / global_res_;
-      else
-        dx = (elevation_[k + 1] - elevation_[k - 1]) * 0.5 / global_res_;
-      if (j == 0)
-        dy = (elevation_[k + nx_] - elevation_[k]) / global_res_;
-      else if (j == ny_ - 1)
-        dy = (elevation_[k] - elevation_[k - nx_]) / global_res_;
-      else
-        dy = (elevation_[k + nx_] - elevation_[k - nx_]) * 0.5 / global_res_;
-      slope_[k] = std::atan(std::sqrt(dx * dx + dy * dy));
-
-      // calculateNominalCost (:217-293)
-      const uint32_t t = terrain_[k];
-      if (t == 0) {
-        raw_cost_[k] = cmax;
-        is_obstacle_[k] = 1;
-      } else if (range == 1) {
-        double cdef = cost_lutable[t * num_locs];
-        for (int m = 0; m < num_locs; ++m) cdef = std::min(cdef, cost_lutable[t * num_locs + m]);
-        raw_cost_[k] = std::max(raw_cost_[k], cdef);
-      } else {
-        const double si = slope_[k] * 180 / M_PI / (slope_range_.back() - slope_range_.front()) *
-                          (double)(slope_range_.size() - 1);
-        if (si > (double)(slope_range_.size() - 1)) {
-          raw_cost_[k] = cmax;
-          is_obstacle_[k] = 1;
-        } else {
-          const double smin = std::floor(si), smax = std::ceil(si);
-          double cdef = cmax;
-          if (num_locs > 1) {
-            for (int m = 1; m < num_locs; ++m) {
-              const double c1 = cost_lutable[t * range * num_locs + m * range + (int)smin];
-              const double c2 = cost_lutable[t * range * num_locs + m * range + (int)smax];
-              const double cc = c1 + (c2 - c1) * (si - smin);
-              if (cc < cdef) {
-                cdef = cc;
-                raw_cost_[k] = std::max(raw_cost_[k], cdef);
-                loc_mode_[k] = m;
-              }
-            }
-          } else {
-            const double c1 = cost_lutable[t * range + (int)smin];
-            const double c2 = cost_lutable[t * range + (int)smax];
-            cdef = c1 + (c2 - c1) * (si - smin);
-            raw_cost_[k] = std::max(raw_cost_[k], cdef);
-            loc_mode_[k] = 0;
-          }
-        }
-      }
       if (is_obstacle_[k]) {
         traff_[k] = 0.0;
         hazard_[k] = 1.0;
       }
     }
-  }
-  // smoothCost (:297-308): own previous cost + neighbours' raw_cost
   for (unsigned j = 0; j < ny_; ++j)
-    for (unsigned i = 0; i < nx_; ++i) {
-      const uint64_t k = idx(i, j);
-      double csum = cost_[k], n = 5;
-      if (j == 0) n--; else csum += raw_cost_[k - nx_];
-      if (i == 0) n--; else csum += raw_cost_[k - 1];
-      if (i == nx_ - 1) n--; else csum += raw_cost_[k + 1];
-      if (j == ny_ - 1) n--; else csum += raw_cost_[k + nx_];
-      cost_[k] = csum / n;
-    }
+    for (unsigned i = 0; i < nx_; ++i) smoothCost(i, j);
   markDirty(0, ny_);
   return true;
+}
+
+// :186-210 (off-grid neighbours: one-sided differences; a 1-wide axis reads
+// slope 0 there instead of the reference's NULL dereference)
+void DyMuPathPlanner::calculateSlope(unsigned i, unsigned j) {
+  if (i >= nx_ || j >= ny_) return;
+  const uint64_t k = idx(i, j);
+  double dx = 0, dy = 0;
+  if (nx_ > 1) {
+    if (i == 0)
+      dx = (elevation_[k + 1] - elevation_[k]) / global_res_;
+    else if (i == nx_ - 1)
+      dx = (elevation_[k] - elevation_[k - 1]) / global_res_;
+    else
+      dx = (elevation_[k + 1] - elevation_[k - 1]) * 0.5 / global_res_;
+  }
+  if (ny_ > 1) {
+    if (j == 0)
+      dy = (elevation_[k + nx_] - elevation_[k]) / global_res_;
+    else if (j == ny_ - 1)
+      dy = (elevation_[k] - elevation_[k - nx_]) / global_res_;
+    else
+      dy = (elevation_[k + nx_] - elevation_[k - nx_]) * 0.5 / global_res_;
+  }
+  slope_[k] = std::atan(std::sqrt(dx * dx + dy * dy));
+}
+
+// :217-293 (Cmax recomputed per call, as there)
+void DyMuPathPlanner::calculateNominalCost(unsigned i, unsigned j, int range, int numLocs) {
+  if (i >= nx_ || j >= ny_ || cost_lutable.empty()) return;
+  nominalCost(i, j, range, numLocs, *std::max_element(cost_lutable.begin(), cost_lutable.end()));
+}
+
+// Q2: locomotion mode 0 is skipped when there are several; Q3: the neighbours'
+// "Cmax" loops never run (isObstacle was just set); Q4: range == 1 indexes the
+// LUT as terrain * numLocs + m.  A terrain class the LUT does not cover (an
+// out-of-bounds read in the reference) makes the cell an obstacle, as the
+// device kernel does (cost_kernels.hip).
+void DyMuPathPlanner::nominalCost(unsigned i, unsigned j, int range, int num_locs, double cmax) {
+  const uint64_t k = idx(i, j);
+  const uint32_t t = terrain_[k];
+  const size_t nl = cost_lutable.size();
+  auto lut = [&](size_t q) { return q < nl ? cost_lutable[q] : cmax; };
+  if (t == 0 || (uint64_t)(t + 1) * (uint64_t)range * (uint64_t)num_locs > nl) {
+    raw_cost_[k] = cmax;
+    is_obstacle_[k] = 1;
+  } else if (range == 1) {
+    double cdef = lut((size_t)t * num_locs);
+    for (int m = 0; m < (int)locomotion_modes_.size(); ++m)
+      cdef = std::min(cdef, lut((size_t)t * num_locs + m));
+    raw_cost_[k] = std::max(raw_cost_[k], cdef);
+  } else {
+    const double si = slope_[k] * 180 / M_PI / (slope_range_.back() - slope_range_.front()) *
+                      (double)(slope_range_.size() - 1);
+    if (si > (double)(slope_range_.size() - 1)) {
+      raw_cost_[k] = cmax;
+      is_obstacle_[k] = 1;
+    } else {
+      const double smin = std::floor(si), smax = std::ceil(si);
+      double cdef = cmax;
+      if (num_locs > 1) {
+        for (int m = 1; m < (int)locomotion_modes_.size(); ++m) {
+          const double c1 = lut((size_t)t * range * num_locs + (size_t)m * range + (int)smin);
+          const double c2 = lut((size_t)t * range * num_locs + (size_t)m * range + (int)smax);
+          const double cc = c1 + (c2 - c1) * (si - smin);
+          if (cc < cdef) {
+            cdef = cc;
+            raw_cost_[k] = std::max(raw_cost_[k], cdef);
+            loc_mode_[k] = m;
+          }
+        }
+      } else {
+        const double c1 = lut((size_t)t * range + (int)smin);
+        const double c2 = lut((size_t)t * range + (int)smax);
+        cdef = c1 + (c2 - c1) * (si - smin);
+        raw_cost_[k] = std::max(raw_cost_[k], cdef);
+        loc_mode_[k] = 0;
+      }
+    }
+  }
+}
+
+// :297-308 (Q1: starts from the node's previous cost)
+void DyMuPathPlanner::smoothCost(unsigned i, unsigned j) {
+  if (i >= nx_ || j >= ny_) return;
+  const uint64_t k = idx(i, j);
+  double csum = cost_[k], n = 5;
+  if (j == 0) n--; else csum += raw_cost_[k - nx_];
+  if (i == 0) n--; else csum += raw_cost_[k - 1];
+  if (i == nx_ - 1) n--; else csum += raw_cost_[k + 1];
+  if (j == ny_ - 1) n--; else csum += raw_cost_[k + nx_];
+  cost_[k] = csum / n;
 }
 
 // :322-357

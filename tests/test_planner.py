@@ -359,3 +359,27 @@ def test_decrease_only_window_through_planner(dymu, oracle):
         fin = np.isfinite(Tref)
         assert (np.abs(T[fin] - Tref[fin]) / np.maximum(1, Tref[fin])).max() <= RTOL
     assert visits["down"] <= visits["up"]
+
+
+def test_terrain_class_beyond_lut_is_obstacle(dymu, oracle):
+    """A terrain class the LUT does not cover (an out-of-bounds read in the
+    reference, :237-241 / :270-273) becomes an obstacle, on the host as in the
+    device kernel (cost_kernels.hip); every other cell matches the oracle."""
+    from gen_golden import terrain_inputs
+    N = 32
+    elev, terr, lut, slopes = terrain_inputs(N)  # LUT covers terrain 0..2
+    terr = terr.copy()
+    terr[10:14, 10:14] = 3.0
+    p = dymu.Planner()
+    p.initGlobalLayer(1.0, 0.5, N, N)
+    assert p.computeCostMap(lut, slopes, ["Wheel"], elev, terr)
+    G = p.getGlobalCostMatrix()
+    assert (G[10:14, 10:14] == -1.0).all()
+    terr_ok = terr.copy()
+    terr_ok[10:14, 10:14] = 1.0
+    st = oracle.new_state(N, N)
+    oracle.compute_cost_map(st, 1.0, lut, slopes, 1, elev, terr_ok)
+    ref = oracle_global_cost(st)
+    mask = np.ones((N, N), bool)
+    mask[9:15, 9:15] = False  # the block and the ring its raw cost is smoothed into
+    assert np.array_equal(G[mask], ref[mask])
