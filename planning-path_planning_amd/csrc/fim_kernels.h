@@ -56,6 +56,11 @@ struct PassArgs {
                             // after its workgroup started the pass (re-queued as if capped)
   int exact_sqrt;  // kernel 5 (dyn): 1 = correctly rounded sweep sqrt (10 VALU), 0 = one
                    // Goldschmidt step (5 VALU, <= 36 ulp)
+  // convergence mailbox: when set, block 0 stores (report_seq << 32) | n_active -- the
+  // tiles queued by the previous pass -- into this word of host-coherent pinned memory,
+  // so the host learns a batch's outcome without a stream synchronisation
+  unsigned long long* report;
+  uint32_t report_seq;
 };
 
 constexpr int kBins = 64;  // v4/v5 key histogram bins

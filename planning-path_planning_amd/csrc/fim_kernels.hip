@@ -306,6 +306,14 @@ __device__ __forceinline__ int rb_sweeps(double* img, int sr, int sb, double fr,
   return sweeps;
 }
 
+// the convergence mailbox (PassArgs::report): a system-scope vector store into
+// host-coherent memory, visible to a polling host thread while the stream runs
+__device__ __forceinline__ void report_pending(const PassArgs& a, uint32_t n_active) {
+  if (a.report)
+    __hip_atomic_store(a.report, ((unsigned long long)a.report_seq << 32) | n_active,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(256) void k_fim_pass_rb(PassArgs a) {
   __shared__ uint32_t s_q[QCAP];
   __shared__ uint32_t s_pref[kShards + 1];
@@ -341,6 +349,7 @@ __global__ __launch_bounds__(256) void k_fim_pass_rb(PassArgs a) {
       atomicAdd(&a.stats[kStatPasses], 1ull);
       atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
     }
+    if (tid == 0) report_pending(a, n_active);
   }
 
   unsigned long long my_visits = 0, my_sweeps = 0;
@@ -922,6 +931,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_prio(PassArgs a) {
         atomicAdd(&a.stats[kStatPasses], 1ull);
         atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
       }
+      report_pending(a, n_active);
     }
   }
 
@@ -1126,6 +1136,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
         atomicAdd(&a.stats[kStatPasses], 1ull);
         atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
       }
+      report_pending(a, n_active);
     }
   }
 
