@@ -139,6 +139,9 @@ int dymu_scatter(dymu_ctx* ctx, double* dT, uint32_t nx, uint64_t ld, const uint
  *   dymu_dom_begin -> repeat { dymu_dom_run(K passes); exchange boundary rows
  *   (RCCL); dymu_dom_merge_ghosts(received rows) } until the all-reduced
  *   pending count is 0 -> dymu_dom_finish.
+ * or, on kernel-5 slabs (include/dymu_dist.h's native loop):
+ *   dymu_dom_begin -> repeat { dymu_dom_round(K passes, merging the rows the
+ *   previous exchange received); exchange boundary rows } until 0 -> finish.
  * All calls except dymu_dom_pending / dymu_dom_finish are asynchronous on
  * `stream`. */
 typedef struct dymu_domain {
@@ -167,6 +170,24 @@ int dymu_dom_merge_ghosts(dymu_ctx* ctx, const double* new_lo, const double* new
  * int32, required) receives the number of tiles queued for the next pass. */
 int dymu_dom_exchange(dymu_ctx* ctx, const double* new_lo, const double* new_hi,
                       int32_t* d_total, void* stream);
+/* One round with the ghost merge inside the passes: `passes` (>= 2) FIM passes,
+ * the first of which min-merges the received rows (device, nx doubles, or NULL)
+ * into the ghost rows; *d_total (device int32) receives the tiles queued for
+ * the round's first pass plus those queued for its second (0 on every rank =
+ * fixed point).  Replaces dymu_dom_run + dymu_dom_exchange for the rows of the
+ * PREVIOUS round (one launch per round fewer).  Only for domains on kernel 5:
+ * DYMU_ERR_STATE otherwise; dymu_dom_round_supported says which (1 / 0). */
+int dymu_dom_round_supported(dymu_ctx* ctx, uint32_t passes);
+int dymu_dom_round(dymu_ctx* ctx, uint32_t passes, const double* new_lo, const double* new_hi,
+                   int32_t* d_total, void* stream);
+/* Arm a post for the next launched pass: its block 0 stores *d_src (device
+ * int32) into the context's host-coherent mailbox with sequence *seq, so the
+ * host can read a device value (the all-reduced count) without a copy or a
+ * stream synchronisation; dymu_dom_wait_post spins for it (timeout_s > 0:
+ * DYMU_ERR_HIP after that long).  DYMU_ERR_STATE without a mailbox. */
+int dymu_dom_post(dymu_ctx* ctx, const int32_t* d_src, uint32_t* seq);
+int dymu_dom_wait_post(dymu_ctx* ctx, uint32_t seq, double timeout_s, int32_t* value,
+                       void* stream);
 /* Tiles queued for the next pass (synchronises `stream`). */
 int dymu_dom_pending(dymu_ctx* ctx, void* stream, uint64_t* pending);
 /* End the domain solve; fills stats (passes, visits, sweeps). */

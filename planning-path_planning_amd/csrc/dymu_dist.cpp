@@ -11,7 +11,10 @@
 //      pinned host memory + event.
 // The host reads the previous check's count after queueing the current one, so
 // it never drains the device queue; up to two check intervals of (empty) rounds
-// run after convergence.
+// run after convergence.  With kernel-5 slabs (dymu_dom_round) the received rows
+// are instead merged by the next round's first pass -- no exchange launch -- and
+// the all-reduced count reaches the host through the engine's mailbox: the next
+// round's first pass stores it into host-coherent memory (no copy, no event).
 //
 // Why one stream and no overlap: the pass kernel is one 1024-thread workgroup
 // per CU at full register use, back to back, so a kernel on a second stream
@@ -159,12 +162,17 @@ void pipe_free(Pipe* p) {
 // Host wait on an event queued behind RCCL work, bounded: a peer that died or
 // left the collective sequence would otherwise block this rank forever.
 // DYMU_DIST_TIMEOUT_S (default 300 s) bounds one wait.
-int wait_event(hipEvent_t ev, std::string* err) {
+double dist_timeout_s() {
   static const double limit_s = [] {
     const char* kv = std::getenv("DYMU_DIST_TIMEOUT_S");
     const double v = kv ? std::atof(kv) : 0.0;
     return v > 0.0 ? v : 300.0;
   }();
+  return limit_s;
+}
+
+int wait_event(hipEvent_t ev, std::string* err) {
+  const double limit_s = dist_timeout_s();
   const auto t0 = std::chrono::steady_clock::now();
   for (unsigned spin = 0;; ++spin) {
     const hipError_t e = hipEventQuery(ev);
@@ -255,15 +263,22 @@ int dist_rounds(dymu_dist* d, const Slab& s, uint32_t nx, uint32_t ny, uint32_t 
   const Pipe& p = d->pipe;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const uint64_t cap = max_rounds(nx, ny, K) + 2 * kCheckEvery;
+  // fused: the rows received after round m are merged by round m+1's first pass
+  // (dymu_dom_round) instead of a k_exchange launch after the transfer
+  const bool fused = dymu_dom_round_supported(d->ctx, K) == 1;
+  bool mail = true;  // checks read through the context's mailbox while it has one
+  uint32_t prev_seq = 0;
   uint64_t m = 0, checks = 0;
-  bool done = false;
+  bool done = false, have_rows = false;
   for (; !done; ++m) {
     if (m >= cap) return fail(err, "dymu_dist_solve", "exchange-round cap reached",
                               DYMU_ERR_NOT_CONVERGED);
     const bool check = (m % kCheckEvery) == kCheckEvery - 1;
     const int par = (int)(checks & 1);
-    int rc = dymu_dom_run(d->ctx, K, stream);
-    if (rc) return fail(err, "dymu_dom_run", dymu_last_error(d->ctx), rc);
+    int rc = fused ? dymu_dom_round(d->ctx, K, have_rows && s.lo ? p.r(0) : nullptr,
+                                    have_rows && s.hi ? p.r(1) : nullptr, p.tot(par), stream)
+                   : dymu_dom_run(d->ctx, K, stream);
+    if (rc) return fail(err, fused ? "dymu_dom_round" : "dymu_dom_run", dymu_last_error(d->ctx), rc);
     if (s.lo || s.hi) {
       DNCCL(err, ncclGroupStart());
       if (s.lo) {
@@ -276,18 +291,40 @@ int dist_rounds(dymu_dist* d, const Slab& s, uint32_t nx, uint32_t ny, uint32_t 
       }
       DNCCL(err, ncclGroupEnd());
     }
-    rc = dymu_dom_exchange(d->ctx, s.lo ? p.r(0) : nullptr, s.hi ? p.r(1) : nullptr, p.tot(par),
-                           stream);
-    if (rc) return fail(err, "dymu_dom_exchange", dymu_last_error(d->ctx), rc);
+    have_rows = true;
+    if (!fused) {
+      rc = dymu_dom_exchange(d->ctx, s.lo ? p.r(0) : nullptr, s.hi ? p.r(1) : nullptr, p.tot(par),
+                             stream);
+      if (rc) return fail(err, "dymu_dom_exchange", dymu_last_error(d->ctx), rc);
+    }
     if (!check) continue;
     DNCCL(err, ncclAllReduce(p.tot(par), p.sum(par), 1, ncclInt32, ncclSum, d->comm, st));
-    DHIP(err, hipMemcpyAsync(d->h_sum + par, p.sum(par), sizeof(int32_t), hipMemcpyDeviceToHost,
-                             st));
-    DHIP(err, hipEventRecord(d->ev[par], st));
-    if (checks >= 1) {  // the previous check's global count; this one stays queued meanwhile
-      rc = wait_event(d->ev[par ^ 1], err);
-      if (rc) return rc;
-      done = d->h_sum[par ^ 1] == 0;
+    if (mail) {  // the next round's first pass posts the sum; read the previous check's
+      uint32_t seq = 0;
+      rc = dymu_dom_post(d->ctx, p.sum(par), &seq);
+      if (rc == DYMU_ERR_STATE && checks == 0) {
+        mail = false;
+      } else if (rc) {
+        return fail(err, "dymu_dom_post", dymu_last_error(d->ctx), rc);
+      } else {
+        if (checks >= 1) {
+          int32_t v = 0;
+          rc = dymu_dom_wait_post(d->ctx, prev_seq, dist_timeout_s(), &v, stream);
+          if (rc) return fail(err, "dymu_dom_wait_post", dymu_last_error(d->ctx), DYMU_ERR_RCCL);
+          done = v == 0;
+        }
+        prev_seq = seq;
+      }
+    }
+    if (!mail) {
+      DHIP(err, hipMemcpyAsync(d->h_sum + par, p.sum(par), sizeof(int32_t),
+                               hipMemcpyDeviceToHost, st));
+      DHIP(err, hipEventRecord(d->ev[par], st));
+      if (checks >= 1) {  // the previous check's global count; this one stays queued meanwhile
+        rc = wait_event(d->ev[par ^ 1], err);
+        if (rc) return rc;
+        done = d->h_sum[par ^ 1] == 0;
+      }
     }
     ++checks;
   }
@@ -399,6 +436,11 @@ int dymu_vdist_solve(dymu_ctx* const* ctxs, int world, const double* const* F_sl
   // the schedule of dymu_dist_solve with every rank's work serialised on one
   // stream: device-to-device row copies for RCCL P2P, a host sum for the
   // all-reduce
+  // fused rounds (kernel 5 slabs): as dist_rounds, the copied rows are merged by
+  // each rank's next round
+  bool fused = true;
+  for (int r = 0; r < world; ++r) fused = fused && dymu_dom_round_supported(ctxs[r], K) == 1;
+  bool have_rows = false;
   for (; !done && rc == DYMU_OK; ++m) {
     if (m >= cap) {
       rc = DYMU_ERR_NOT_CONVERGED;
@@ -406,7 +448,10 @@ int dymu_vdist_solve(dymu_ctx* const* ctxs, int world, const double* const* F_sl
     }
     const bool check = (m % kCheckEvery) == kCheckEvery - 1;
     const int par = (int)(checks & 1);
-    for (int r = 0; r < world && rc == DYMU_OK; ++r) rc = dymu_dom_run(ctxs[r], K, stream);
+    for (int r = 0; r < world && rc == DYMU_OK; ++r)
+      rc = fused ? dymu_dom_round(ctxs[r], K, have_rows && s[r].lo ? p[r].r(0) : nullptr,
+                                  have_rows && s[r].hi ? p[r].r(1) : nullptr, p[r].tot(par), stream)
+                 : dymu_dom_run(ctxs[r], K, stream);
     if (rc) break;
     for (int r = 0; r < world; ++r) {  // rank r-1's last row / rank r+1's first row
       if (s[r].lo)
@@ -416,9 +461,11 @@ int dymu_vdist_solve(dymu_ctx* const* ctxs, int world, const double* const* F_sl
         DHIP(nullptr, hipMemcpyAsync(p[r].r(1), s[r + 1].row(0), sizeof(double) * nx,
                                      hipMemcpyDeviceToDevice, st));
     }
+    have_rows = true;
     for (int r = 0; r < world && rc == DYMU_OK; ++r) {
-      rc = dymu_dom_exchange(ctxs[r], s[r].lo ? p[r].r(0) : nullptr,
-                             s[r].hi ? p[r].r(1) : nullptr, p[r].tot(par), stream);
+      if (!fused)
+        rc = dymu_dom_exchange(ctxs[r], s[r].lo ? p[r].r(0) : nullptr,
+                               s[r].hi ? p[r].r(1) : nullptr, p[r].tot(par), stream);
       if (rc == DYMU_OK && check &&
           hipMemcpyAsync(h_tot + par * world + r, p[r].tot(par), sizeof(int32_t),
                          hipMemcpyDeviceToHost, st) != hipSuccess)

@@ -59,6 +59,9 @@ struct dymu_ctx {
   unsigned long long* h_mail = nullptr;  // pinned, host-coherent: (seq << 32) | pending
   unsigned long long* d_mail = nullptr;  // its device address
   uint32_t mail_seq = 0;
+  // a post armed by dymu_dom_post for the next launched pass (sharded loop)
+  const int32_t* arm_src = nullptr;
+  uint32_t arm_seq = 0;
   int prio_debug = 0;        // v4: print the state after the first N passes (DYMU_PRIO_DEBUG)
 
   // tile workspace
@@ -196,6 +199,8 @@ constexpr uint64_t kPassSlack = 128;
 // above every epoch this one used, so no tile_epoch entry can block them.
 void dom_retire(dymu_ctx* c) {
   auto& D = c->dom;
+  c->arm_seq = 0;  // a post armed for a pass that will not run
+  c->arm_src = nullptr;
   if (!D.live) return;
   c->epoch_base = D.eb + (uint32_t)D.p + 4u;
   D.live = false;
@@ -344,6 +349,12 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st, uint32_t report_seq = 0)
     if (k == 0 && report_seq) {
       a.report = c->d_mail;
       a.report_seq = report_seq;
+    } else if (c->arm_seq) {
+      a.report = c->d_mail;
+      a.report_seq = c->arm_seq;
+      a.report_src = c->arm_src;
+      c->arm_seq = 0;
+      c->arm_src = nullptr;
     }
     const bool tr = is_prio(D.variant) && c->prio_trace >= 0 && p == (uint64_t)c->prio_trace;
     if (tr) {
@@ -368,6 +379,7 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st, uint32_t report_seq = 0)
                              : launch_pass_rb(a, D.blocks, st, e0, e1));
     ++D.launches;
     a.report = nullptr;
+    a.report_src = nullptr;
     if (tr) {
       a.trace = nullptr;
       std::vector<unsigned long long> h((size_t)kTracePts * D.blocks);
@@ -455,6 +467,38 @@ int dom_exchange(dymu_ctx* c, const double* lo, const double* hi, int32_t* d_tot
                           is_prio(D.variant) ? prio_base(c, p % 3) : nullptr,
                           is_prio(D.variant) ? prio_delta(c) : nullptr, c->d_xchg, d_total, st));
   return DYMU_OK;
+}
+
+// One round of the sharded loop with the ghost merge inside the passes (kernel 5,
+// K >= 2): the first pass min-merges the rows received after the previous round
+// and queues the tiles under improved columns for the second; the second pass
+// writes *d_total = tiles queued for the first + for the second pass.  0 on every
+// rank is the fixed point: nothing was queued after the previous round, and the
+// rows it produced improved no ghost.
+bool dom_round_ok(const dymu_ctx* c, uint64_t K) {
+  return c->dom.live && c->dom.variant == 5 && K >= 2;
+}
+
+int dom_round(dymu_ctx* c, uint64_t K, const double* lo, const double* hi, int32_t* d_total,
+              hipStream_t st) {
+  auto& D = c->dom;
+  if (!dom_round_ok(c, K)) return DYMU_ERR_STATE;
+  if (!d_total || (lo && !D.a.ghost_lo) || (hi && !D.a.ghost_hi)) return DYMU_ERR_ARG;
+  uint32_t* scratch = reinterpret_cast<uint32_t*>(c->d_scratch + 7);
+  D.a.merge_lo = lo;
+  D.a.merge_hi = hi;
+  D.a.tot_save = scratch;
+  int rc = dom_launch(c, 1, st);
+  D.a.merge_lo = D.a.merge_hi = nullptr;
+  D.a.tot_save = nullptr;
+  if (rc) return rc;
+  D.a.tot_prev = scratch;
+  D.a.tot_out = d_total;
+  rc = dom_launch(c, 1, st);
+  D.a.tot_prev = nullptr;
+  D.a.tot_out = nullptr;
+  if (rc) return rc;
+  return dom_launch(c, K - 2, st);
 }
 
 int dom_finish(dymu_ctx* c, hipStream_t st, dymu_stats* stats, double ms) {
@@ -556,7 +600,7 @@ int converge(dymu_ctx* c, hipStream_t st, dymu_stats* stats, const ProbeCells* p
 // Posts carry increasing sequence numbers; this returns the first one seen at or
 // after seq (its number in *seen when seen is given).
 int wait_mail(dymu_ctx* c, hipStream_t st, uint32_t seq, uint32_t* pending,
-              uint32_t* seen = nullptr) {
+              uint32_t* seen = nullptr, double timeout_s = 0.0) {
   auto arrived = [&](unsigned long long v) {
     if ((int32_t)((uint32_t)(v >> 32) - seq) < 0) return false;
     *pending = (uint32_t)v;
@@ -570,6 +614,11 @@ int wait_mail(dymu_ctx* c, hipStream_t st, uint32_t seq, uint32_t* pending,
     if (arrived(__atomic_load_n(c->h_mail, __ATOMIC_ACQUIRE))) return DYMU_OK;
     if ((spin & 255) == 0 && clk::now() >= next_query) {
       next_query += std::chrono::milliseconds(5);
+      if (timeout_s > 0.0 &&
+          std::chrono::duration<double>(clk::now() - t0).count() > timeout_s) {
+        c->last_error = "convergence mailbox: timed out waiting for a post";
+        return DYMU_ERR_HIP;
+      }
       const hipError_t e = hipStreamQuery(st);
       if (e == hipSuccess) {  // drained: the post, if made, is visible now
         if (arrived(__atomic_load_n(c->h_mail, __ATOMIC_ACQUIRE))) return DYMU_OK;
@@ -1129,6 +1178,38 @@ int dymu_dom_exchange(dymu_ctx* c, const double* new_lo, const double* new_hi,
   if (!c) return DYMU_ERR_ARG;
   HIPC(c, hipSetDevice(c->device));
   return dom_exchange(c, new_lo, new_hi, d_total, pick_stream(c, stream));
+}
+
+int dymu_dom_round_supported(dymu_ctx* c, uint32_t passes) {
+  return c && dom_round_ok(c, passes) ? 1 : 0;
+}
+
+int dymu_dom_round(dymu_ctx* c, uint32_t passes, const double* new_lo, const double* new_hi,
+                   int32_t* d_total, void* stream) {
+  if (!c) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  return dom_round(c, passes, new_lo, new_hi, d_total, pick_stream(c, stream));
+}
+
+int dymu_dom_post(dymu_ctx* c, const int32_t* d_src, uint32_t* seq) {
+  if (!c || !d_src || !seq) return DYMU_ERR_ARG;
+  if (!c->d_mail || !c->dom.live) return DYMU_ERR_STATE;
+  if (++c->mail_seq == 0) c->mail_seq = 1;
+  c->arm_src = d_src;
+  c->arm_seq = c->mail_seq;
+  *seq = c->mail_seq;
+  return DYMU_OK;
+}
+
+int dymu_dom_wait_post(dymu_ctx* c, uint32_t seq, double timeout_s, int32_t* value,
+                       void* stream) {
+  if (!c || !value || seq == 0) return DYMU_ERR_ARG;
+  if (!c->d_mail) return DYMU_ERR_STATE;
+  uint32_t v = 0;
+  const int rc = wait_mail(c, pick_stream(c, stream), seq, &v, nullptr, timeout_s);
+  if (rc) return rc;
+  *value = (int32_t)v;
+  return DYMU_OK;
 }
 
 int dymu_dom_pending(dymu_ctx* c, void* stream, uint64_t* pending) {

@@ -61,6 +61,15 @@ struct PassArgs {
   // so the host learns a batch's outcome without a stream synchronisation
   unsigned long long* report;
   uint32_t report_seq;
+  const int32_t* report_src;  // post *report_src instead of the pass's count (sharded loop)
+  // ---- kernel 5, sharded rounds (dom_round) ----
+  // received neighbour rows (nx doubles, device) min-merged into the ghost rows by this
+  // pass; the tiles under improved columns are queued for the NEXT pass
+  const double* merge_lo;
+  const double* merge_hi;
+  uint32_t* tot_save;       // block 0 stores the pass's count here ...
+  const uint32_t* tot_prev;  // ... and a later pass stores *tot_prev + its count
+  int32_t* tot_out;          //     into *tot_out (the round's termination count)
 };
 
 constexpr int kBins = 64;  // v4/v5 key histogram bins

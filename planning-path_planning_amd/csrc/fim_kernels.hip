@@ -309,9 +309,11 @@ __device__ __forceinline__ int rb_sweeps(double* img, int sr, int sb, double fr,
 // the convergence mailbox (PassArgs::report): a system-scope vector store into
 // host-coherent memory, visible to a polling host thread while the stream runs
 __device__ __forceinline__ void report_pending(const PassArgs& a, uint32_t n_active) {
-  if (a.report)
-    __hip_atomic_store(a.report, ((unsigned long long)a.report_seq << 32) | n_active,
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (a.report) {
+    const uint32_t v = a.report_src ? (uint32_t)*a.report_src : n_active;
+    __hip_atomic_store(a.report, ((unsigned long long)a.report_seq << 32) | v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_fim_pass_rb(PassArgs a) {
@@ -1073,7 +1075,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   __shared__ uint32_t s_q[QCAP];
   __shared__ uint32_t s_pref[kShards + 1];
   __shared__ uint32_t s_hout[kBins];
-  __shared__ uint32_t s_nq, s_base, s_next;
+  __shared__ uint32_t s_nq, s_base, s_next, s_merge;
   __shared__ int s_bstar;
   __shared__ unsigned long long s_visits, s_sweeps, s_minout, s_defer;
   __shared__ unsigned long long s_ek[WPB][4];
@@ -1115,6 +1117,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       s_bstar = (a.target > 0 && n > target && m) ? (int)__ffsll((long long)m) - 1 : kBins;
       s_nq = 0;
       s_next = 0;
+      s_merge = 0;
       s_visits = 0;
       s_sweeps = 0;
       s_defer = 0;
@@ -1137,6 +1140,8 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
         atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
       }
       report_pending(a, n_active);
+      if (a.tot_save) *a.tot_save = n_active;
+      if (a.tot_out) *a.tot_out = (int32_t)(*a.tot_prev + n_active);
     }
   }
 
@@ -1215,6 +1220,39 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       if (tid == 0) trace[8] = __builtin_amdgcn_s_memrealtime();
     }
     first = false;
+  }
+  if (a.merge_lo || a.merge_hi) {  // uniform; the first wave out of the loop merges
+    uint32_t mine = 0;
+    if (lane == 0) mine = atomicAdd(&s_merge, 1u) == 0u;
+    if (__builtin_amdgcn_readfirstlane(mine)) {
+      // this workgroup's share of the columns (a whole number of 16-wide tiles): min-merge
+      // the received rows into the ghost rows, queue the tile under each improved column
+      // group with the smallest improved value as its key (as k_merge_ghosts)
+      const int64_t cw = (((int64_t)a.nx + gridDim.x - 1) / gridDim.x + 15) & ~(int64_t)15;
+      const int64_t m0 = (int64_t)blockIdx.x * cw;
+      const int64_t m1 = min((int64_t)a.nx, m0 + cw);
+      for (int side = 0; side < 2; ++side) {
+        const double* src = side == 0 ? a.merge_lo : a.merge_hi;
+        if (!src) continue;
+        double* gh = a.T + (side == 0 ? -a.ld : a.ny * a.ld);
+        const uint32_t trow = side == 0 ? 0u : (uint32_t)(a.nty - 1);
+        for (int64_t k0 = m0; k0 < m1; k0 += 64) {
+          const int64_t k = k0 + lane;
+          double w = dinf();
+          if (k < m1) {
+            const double v = src[k];
+            if (v < gh[k]) {
+              gh[k] = v;
+              w = v;
+            }
+          }
+#pragma unroll
+          for (int o = 8; o > 0; o >>= 1) w = vmin64(w, __shfl_xor(w, o));
+          if ((lane & 15) == 0 && k < m1 && w < dinf())
+            enqueue(trow * (uint32_t)a.ntx + (uint32_t)(k >> 4), dbits(w));
+        }
+      }
+    }
   }
   if (trace && tid == 0) trace[3] = __builtin_amdgcn_s_memrealtime();
   if (lane == 0 && (my_visits || my_defer)) {

@@ -118,6 +118,11 @@ FIM_SYMBOLS = {
     "dymu_dom_merge_ghosts": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dymu_dom_pending": (_i32, [_vp, _vp, ctypes.POINTER(_u64)]),
     "dymu_dom_exchange": (_i32, [_vp, _vp, _vp, _vp, _vp]),
+    "dymu_dom_round_supported": (_i32, [_vp, _u32]),
+    "dymu_dom_round": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp]),
+    "dymu_dom_post": (_i32, [_vp, _vp, ctypes.POINTER(_u32)]),
+    "dymu_dom_wait_post": (_i32, [_vp, _u32, ctypes.c_double, ctypes.POINTER(ctypes.c_int32),
+                                  _vp]),
     "dymu_dom_finish": (_i32, [_vp, _vp, ctypes.POINTER(DymuStats)]),
     "dymu_last_pass_timing": (_i32, [_vp, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_uint64)]),
@@ -167,7 +172,10 @@ def load_fim() -> ctypes.CDLL:
         if not os.path.exists(path):
             raise DymuError(-5, f"HIP extension missing: {path} (run __graft_entry__.build())")
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        ab_build = "DYMU_LIBDIR" in os.environ  # an older A/B build may lack newer symbols
         for name, (res, args) in FIM_SYMBOLS.items():
+            if ab_build and not hasattr(lib, name):
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
