@@ -257,3 +257,27 @@ def test_parity_serpentine_maze(kengine, oracle, N, period):
     Tref, _ = oracle.fmm(F, g)
     assert_parity(r.T, Tref)
     assert r.stats["passes"] > 4 * N // (r.stats["tile_w"] * 2)  # the maze inflates the passes
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+@pytest.mark.parametrize("kernel", [3, 5])
+def test_convergence_check_modes(dymu, oracle, monkeypatch, mode, kernel):
+    """DYMU_PIPELINE 0 (read-back after each batch), 1 (batch posts to the
+    mailbox) and 2 (per-pass posts, 4 passes queued; the default) end on the
+    same fixed point; the empty passes queued after convergence change nothing
+    and are counted as launches, not passes (DESIGN.md s4 "Convergence checks")."""
+    monkeypatch.setenv("DYMU_PIPELINE", mode)
+    nx, ny, g = 640, 512, (100, 400)
+    F = oracle.synth_speed(nx, ny, seed=12, obst_frac=0.04, obst_seed=13, goal=g)
+    eng = dymu.Engine(kernel=kernel, prio_target=64 if kernel == 5 else 0)
+    try:
+        rs = [eng.solve(F, g[0], g[1]) for _ in range(2)]
+    finally:
+        eng.close()
+    Tref, _ = oracle.fmm(F, g)
+    for r in rs:
+        assert_parity(r.T, Tref)
+        assert r.stats["kernel"] == kernel
+        assert r.stats["launches"] >= r.stats["passes"] > 0
+        if mode == "2":  # at most the 4 queued-ahead passes run empty
+            assert r.stats["launches"] <= r.stats["passes"] + 4 + 1
