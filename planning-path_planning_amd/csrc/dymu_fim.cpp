@@ -672,9 +672,16 @@ int converge_pipelined(dymu_ctx* c, hipStream_t st, dymu_stats* stats) {
 // Streaming variant (DYMU_PIPELINE=2): every pass posts, and the host keeps
 // c->max_batch passes queued ahead of the one running -- the overshoot after
 // convergence is at most that many passes.
-int converge_stream(dymu_ctx* c, hipStream_t st, dymu_stats* stats) {
+// probe (priority kernels): the passes also post whether the probe cells are final
+// (PassArgs::probe); the loop stops at the first such post, and *t_probe gets their
+// largest value (+inf if one is unreachable: then the solve runs to the end).  The
+// <= 4 passes queued behind that post only lower values above *t_probe (every key
+// exceeds it), so the cells <= *t_probe are exactly those of converge()'s exit.
+int converge_stream(dymu_ctx* c, hipStream_t st, dymu_stats* stats,
+                    const ProbeCells* probe = nullptr, double* t_probe = nullptr) {
   HIPC(c, hipEventRecord(c->ev0, st));
   auto& D = c->dom;
+  if (probe) D.a.probe = *probe;
   const uint64_t ahead = c->max_batch;
   const uint32_t base = c->mail_seq + 1;  // pass p posts base + p
   auto post_seq = [&](uint64_t p) { uint32_t s = base + (uint32_t)p; return s ? s : 1u; };
@@ -686,7 +693,7 @@ int converge_stream(dymu_ctx* c, hipStream_t st, dymu_stats* stats) {
     rc = wait_mail(c, st, post_seq(running), &pending, &seen);
     if (rc) break;
     running = (uint64_t)(uint32_t)(seen - base);
-    if (pending == 0) break;
+    if ((pending & 0x7FFFFFFFu) == 0 || (pending & 0x80000000u)) break;
     if (running > D.max_passes) {
       c->last_error = "pass cap reached before convergence";
       rc = DYMU_ERR_NOT_CONVERGED;
@@ -696,13 +703,21 @@ int converge_stream(dymu_ctx* c, hipStream_t st, dymu_stats* stats) {
     ++running;
   }
   c->mail_seq = base + (uint32_t)D.p + 1;
+  D.a.probe.n = 0;
   if (rc) {
     dom_retire(c);
     (void)hipStreamSynchronize(st);
     return rc;
   }
   HIPC(c, hipEventRecord(c->ev1, st));
+  if (probe) {
+    HIPC(c, launch_probe(D.a.T, D.a.ld, *probe, nullptr, c->d_scratch + 2, st));
+    HIPC(c, hipMemcpyAsync(c->h_probe, c->d_scratch + 2, 2 * sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, st));
+  }
   HIPC(c, hipEventSynchronize(c->ev1));
+  HIPC(c, hipStreamSynchronize(st));
+  if (probe) std::memcpy(t_probe, &c->h_probe[0], sizeof(double));
   float ms = 0.f;
   HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
   return dom_finish(c, st, stats, ms);
@@ -750,6 +765,8 @@ int solve_until_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uin
   if (rc) return rc;
   const ProbeCells p = start_probe(nx, ny, si, sj);
   *t_closed = __builtin_inf();
+  if (c->pipeline == 2 && c->d_mail && c->opts.passes_per_check <= 0)
+    return converge_stream(c, st, stats, &p, t_closed);
   return converge(c, st, stats, &p, t_closed);
 }
 

@@ -18,6 +18,11 @@ enum StatSlot : int {
   kStatSlots = 8
 };
 
+struct ProbeCells {
+  int64_t ij[5][2];  // (i, j) of the start cell and its in-grid 4-neighbours
+  int n;
+};
+
 struct PassArgs {
   const double* F;  // speed, pitch ld
   double* T;        // total cost, pitch ld (row -1 / row ny are ghost rows when flagged)
@@ -62,6 +67,10 @@ struct PassArgs {
   unsigned long long* report;
   uint32_t report_seq;
   const int32_t* report_src;  // post *report_src instead of the pass's count (sharded loop)
+  // priority kernels, with report: bit 31 of the posted count is set when every queued
+  // tile's key (min key of the input list) exceeds the largest T over these cells -- they
+  // are final (the early exit of dymu_solve_until_device); n = 0: off
+  ProbeCells probe;
   // ---- kernel 5, sharded rounds (dom_round) ----
   // received neighbour rows (nx doubles, device) min-merged into the ghost rows by this
   // pass; the tiles under improved columns are queued for the NEXT pass
@@ -154,10 +163,6 @@ hipError_t launch_theta_state(const unsigned long long* theta_bits, unsigned lon
                               double* base0, hipStream_t st);
 
 // early exit of computeTotalCostMap (update_kernels.hip)
-struct ProbeCells {
-  int64_t ij[5][2];  // (i, j) of the start cell and its in-grid 4-neighbours
-  int n;
-};
 // out[0] = bits of max T over the probe cells, out[1] = *minkey (or +inf bits if null)
 hipError_t launch_probe(const double* T, int64_t ld, const ProbeCells& cells,
                         const unsigned long long* minkey, unsigned long long* out,

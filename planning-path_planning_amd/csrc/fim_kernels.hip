@@ -310,7 +310,16 @@ __device__ __forceinline__ int rb_sweeps(double* img, int sr, int sb, double fr,
 // host-coherent memory, visible to a polling host thread while the stream runs
 __device__ __forceinline__ void report_pending(const PassArgs& a, uint32_t n_active) {
   if (a.report) {
-    const uint32_t v = a.report_src ? (uint32_t)*a.report_src : n_active;
+    uint32_t v = a.report_src ? (uint32_t)*a.report_src : n_active;
+    if (a.probe.n > 0 && a.minkey_in) {  // T, keys >= 0: bit order = value order
+      unsigned long long tmax = 0;
+      for (int k = 0; k < a.probe.n; ++k) {
+        const unsigned long long b =
+            __double_as_longlong(a.T[a.probe.ij[k][1] * a.ld + a.probe.ij[k][0]]);
+        tmax = b > tmax ? b : tmax;
+      }
+      if (*a.minkey_in > tmax) v |= 0x80000000u;
+    }
     __hip_atomic_store(a.report, ((unsigned long long)a.report_seq << 32) | v, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }

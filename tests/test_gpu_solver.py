@@ -281,3 +281,37 @@ def test_convergence_check_modes(dymu, oracle, monkeypatch, mode, kernel):
         assert r.stats["launches"] >= r.stats["passes"] > 0
         if mode == "2":  # at most the 4 queued-ahead passes run empty
             assert r.stats["launches"] <= r.stats["passes"] + 4 + 1
+
+
+@pytest.mark.parametrize("mode", ["0", "2"])
+def test_early_exit_modes(dymu, oracle, monkeypatch, mode):
+    """dymu_solve_until_device with the batch read-back (0) and with the in-kernel
+    probe posted every pass (2): the start and its nb4 are final when it returns,
+    t_closed is their largest value, and every cell <= t_closed holds the oracle
+    FMM value; the per-pass probe stops within the 4 queued passes of the first
+    pass that sees them final."""
+    monkeypatch.setenv("DYMU_PIPELINE", mode)
+    N, g = 1024, (512, 512)
+    F = oracle.synth_speed(N, N, seed=3, obst_frac=0.02, obst_seed=5, goal=g)
+    Tref, _ = oracle.fmm(F, g)
+    eng = dymu.Engine(kernel=5, prio_target=64)
+    dF, dT = eng.alloc(8 * N * N), eng.alloc(8 * N * N)
+    try:
+        eng.h2d(dF, F)
+        for s in ((g[0] + 3, g[1] + 2), (g[0] + 200, g[1] - 100), (1, 1)):
+            tc, st = eng.solve_until_device(dF, dT, N, N, N, g[0], g[1], s[0], s[1])
+            T = np.empty((N, N))
+            eng.d2h(T, dT)
+            cells = [(s[0] + di, s[1] + dj) for di, dj in ((0, 0), (1, 0), (-1, 0), (0, 1), (0, -1))
+                     if 0 <= s[0] + di < N and 0 <= s[1] + dj < N]
+            want = max(Tref[j, i] for i, j in cells)
+            assert abs(tc - want) <= RTOL * max(1.0, want)
+            closed = T <= tc
+            assert all(closed[j, i] for i, j in cells)
+            err = np.abs(T[closed] - Tref[closed]) / np.maximum(1.0, Tref[closed])
+            assert err.max() <= RTOL
+            assert st["passes"] > 0
+    finally:
+        eng.free(dF)
+        eng.free(dT)
+        eng.close()
