@@ -106,6 +106,11 @@ class DyMuPathPlanner {
                       std::vector<std::string> locomotionModes,
                       std::vector<std::vector<double>> elevation,
                       std::vector<std::vector<double>> terrainMap);
+  // the same from row-major nx*ny arrays (the flat C-ABI's path: no per-row copies)
+  bool computeCostMap(const std::vector<double>& cost_data,
+                      const std::vector<double>& slope_values,
+                      const std::vector<std::string>& locomotionModes, const double* elevation,
+                      const double* terrainMap);
 
   // the per-node steps of computeCostMap (src/DyMu.hpp:493-497), by grid index
   void calculateSlope(unsigned i, unsigned j);
@@ -212,6 +217,8 @@ class DyMuPathPlanner {
   // pack F for the dirty rows, upload the rows whose speed changed; returns false
   // when nothing changed, else the bounding box of the changed cells
   bool syncSpeed(unsigned& i0, unsigned& i1, unsigned& j0, unsigned& j1);
+  template <class ERows, class TRows>
+  bool costMapFromRows(const ERows& elev_row, const TRows& terr_row);
   bool propagate(bool early, unsigned si, unsigned sj);
   void replayBand(double t_closed, const std::vector<uint64_t>& band, std::vector<double>& out);
   void gradientNode(unsigned i, unsigned j, double& dnx, double& dny) const;

@@ -11,13 +11,16 @@
 //     on first read (path extraction reads a narrow band around the path) or
 //     all of it for the matrix getters.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <cmath>
 #include <cstdio>
 #include <limits>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
+#include <vector>
 
 #include "DyMu.hpp"
 #include "local_layer.hpp"
@@ -132,6 +135,44 @@ bool DyMuPathPlanner::setCostMap(std::vector<std::vector<double>> cost_map) {
   return true;
 }
 
+namespace {
+
+// Host threads for the per-node loops of computeCostMap: DYMU_HOST_THREADS, else
+// OMP_NUM_THREADS, else the hardware's, at most 64.
+unsigned host_threads() {
+  for (const char* v : {"DYMU_HOST_THREADS", "OMP_NUM_THREADS"})
+    if (const char* kv = std::getenv(v)) {
+      const int t = std::atoi(kv);
+      if (t > 0) return (unsigned)std::min(t, 64);
+    }
+  const unsigned h = std::thread::hardware_concurrency();
+  return h ? std::min(h, 64u) : 1u;
+}
+
+// body(j0, j1) over row ranges of [0, ny) on up to host_threads() threads (at
+// least 64 rows each).  Every loop run this way writes only the node it visits
+// and reads fields no iteration of the same loop writes, so the split changes no
+// value -- the results are those of the reference's single raster loop.
+template <class Body>
+void parallel_rows(unsigned ny, Body&& body) {
+  const unsigned nt = std::max(1u, std::min(host_threads(), ny / 64));
+  if (nt == 1) {
+    body(0u, ny);
+    return;
+  }
+  std::vector<std::thread> pool;
+  pool.reserve(nt - 1);
+  const unsigned step = (ny + nt - 1) / nt;
+  for (unsigned t = 1; t < nt; ++t) {
+    const unsigned j0 = t * step, j1 = std::min(ny, j0 + step);
+    if (j0 < j1) pool.emplace_back([&body, j0, j1] { body(j0, j1); });
+  }
+  body(0u, std::min(ny, step));
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
 // :145-181, with :186-210 (slope), :217-293 (nominal cost) and :297-308
 // (smoothing).  Quirks kept: Q1 smoothing starts from the previous cost; Q2
 // locomotion mode 0 skipped when several modes exist; Q3 the neighbour
@@ -144,35 +185,62 @@ bool DyMuPathPlanner::computeCostMap(std::vector<double> cost_data,
   cost_lutable = cost_data;
   slope_range_ = slope_values;
   locomotion_modes_ = locomotionModes;
-  if (cost_lutable.empty() || slope_range_.empty() || locomotion_modes_.empty()) return false;
   if (elevation.size() != ny_ || terrainMap.size() != ny_) return false;
+  for (unsigned j = 0; j < ny_; ++j)
+    if (elevation[j].size() != nx_ || terrainMap[j].size() != nx_) return false;
+  return costMapFromRows([&](unsigned j) { return elevation[j].data(); },
+                         [&](unsigned j) { return terrainMap[j].data(); });
+}
+
+bool DyMuPathPlanner::computeCostMap(const std::vector<double>& cost_data,
+                                     const std::vector<double>& slope_values,
+                                     const std::vector<std::string>& locomotionModes,
+                                     const double* elevation, const double* terrainMap) {
+  cost_lutable = cost_data;
+  slope_range_ = slope_values;
+  locomotion_modes_ = locomotionModes;
+  if (!elevation || !terrainMap) return false;
+  const uint64_t nx = nx_;
+  return costMapFromRows([=](unsigned j) { return elevation + j * nx; },
+                         [=](unsigned j) { return terrainMap + j * nx; });
+}
+
+template <class ERows, class TRows>
+bool DyMuPathPlanner::costMapFromRows(const ERows& elev_row, const TRows& terr_row) {
+  if (cost_lutable.empty() || slope_range_.empty() || locomotion_modes_.empty()) return false;
   const int range = (int)slope_range_.size();
   const int num_locs = (int)locomotion_modes_.size();
   const double cmax = *std::max_element(cost_lutable.begin(), cost_lutable.end());
-
-  for (unsigned j = 0; j < ny_; ++j) {
-    if (elevation[j].size() != nx_ || terrainMap[j].size() != nx_) return false;
-    for (unsigned i = 0; i < nx_; ++i) {
-      const uint64_t k = idx(i, j);
-      raw_cost_[k] = 0;
-      elevation_[k] = elevation[j][i];
-      terrain_[k] = (i == 0 || j == 0 || i == nx_ - 1 || j == ny_ - 1)
-                        ? 0u
-                        : (uint32_t)terrainMap[j][i];
-    }
-  }
-  for (unsigned j = 0; j < ny_; ++j)
-    for (unsigned i = 0; i < nx_; ++i) {
-      calculateSlope(i, j);
-      nominalCost(i, j, range, num_locs, cmax);
-      const uint64_t k = idx(i, j);
-      if (is_obstacle_[k]) {
-        traff_[k] = 0.0;
-        hazard_[k] = 1.0;
+  parallel_rows(ny_, [&](unsigned j0, unsigned j1) {
+    for (unsigned j = j0; j < j1; ++j) {
+      const double* e = elev_row(j);
+      const double* t = terr_row(j);
+      for (unsigned i = 0; i < nx_; ++i) {
+        const uint64_t k = idx(i, j);
+        raw_cost_[k] = 0;
+        elevation_[k] = e[i];
+        terrain_[k] = (i == 0 || j == 0 || i == nx_ - 1 || j == ny_ - 1) ? 0u : (uint32_t)t[i];
       }
     }
-  for (unsigned j = 0; j < ny_; ++j)
-    for (unsigned i = 0; i < nx_; ++i) smoothCost(i, j);
+  });
+  // slope reads the elevation only; the nominal cost its own node
+  parallel_rows(ny_, [&](unsigned j0, unsigned j1) {
+    for (unsigned j = j0; j < j1; ++j)
+      for (unsigned i = 0; i < nx_; ++i) {
+        calculateSlope(i, j);
+        nominalCost(i, j, range, num_locs, cmax);
+        const uint64_t k = idx(i, j);
+        if (is_obstacle_[k]) {
+          traff_[k] = 0.0;
+          hazard_[k] = 1.0;
+        }
+      }
+  });
+  // smoothing writes cost and reads only raw costs (Q1: its own previous cost)
+  parallel_rows(ny_, [&](unsigned j0, unsigned j1) {
+    for (unsigned j = j0; j < j1; ++j)
+      for (unsigned i = 0; i < nx_; ++i) smoothCost(i, j);
+  });
   markDirty(0, ny_);
   return true;
 }

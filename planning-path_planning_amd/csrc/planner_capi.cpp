@@ -103,10 +103,9 @@ int dymu_planner_compute_cost_map(dymu_planner* p, const double* lut, int lut_le
   return guarded([&] {
     std::vector<std::string> modes;
     for (int k = 0; k < n_locs; ++k) modes.emplace_back(loc_modes[k] ? loc_modes[k] : "");
-    const unsigned nx = p->pl.sizeX(), ny = p->pl.sizeY();
     return (int)p->pl.computeCostMap(std::vector<double>(lut, lut + lut_len),
                                      std::vector<double>(slopes, slopes + n_slopes), modes,
-                                     to_rows(elevation, nx, ny), to_rows(terrain, nx, ny));
+                                     elevation, terrain);
   });
 }
 

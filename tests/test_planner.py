@@ -21,7 +21,7 @@ def oracle_global_cost(st):
     return np.where(st["is_obstacle"] != 0, -1.0, c)
 
 
-@pytest.mark.parametrize("res,N", [(0.5, 128), (1.0, 33)])
+@pytest.mark.parametrize("res,N", [(0.5, 128), (1.0, 33), (0.5, 700)])
 def test_compute_cost_map_bitwise(dymu, oracle, res, N):
     elev, terr, lut, slopes = terrain_inputs(N)
     p = dymu.Planner()

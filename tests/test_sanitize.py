@@ -14,7 +14,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FLAGS = ["-g", "-O1", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
-         "-fno-omit-frame-pointer", "-ffp-contract=off"]
+         "-fno-omit-frame-pointer", "-ffp-contract=off", "-pthread"]
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs gcc/g++")
