@@ -261,7 +261,7 @@ class DyMuPathPlanner {
 
   // engine and its device-resident map (pitch nx_)
   dymu_ctx* ctx_ = nullptr;
-  dymu_opts opts_{-1, 0, 0, 0, 0, 0, 0, 0};
+  dymu_opts opts_{-1, 0, 0, 0, 0, 0, 0, 0, 0};
   dymu_stats stats_{};
   double* dF_ = nullptr;
   double* dT_ = nullptr;

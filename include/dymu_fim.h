@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DYMU_ABI_VERSION 4
+#define DYMU_ABI_VERSION 5
 
 typedef enum dymu_status {
   DYMU_OK = 0,
@@ -66,6 +66,10 @@ typedef struct dymu_opts {
                            Goldschmidt step folded into the candidate, <= 36 ulp of the
                            reference candidate, solve error vs the reference FMM unchanged
                            (<= 6e-15 rel) */
+  int deterministic;    /* 1 = bit-reproducible maps: kernel 5 with checkerboard passes (a
+                           pass relaxes tiles of one colour only, so no tile reads a halo
+                           another wave is writing) and no sweep deadline; ~2x the passes.
+                           0 = default (the last ulps depend on the schedule) */
 } dymu_opts;
 
 typedef struct dymu_stats {

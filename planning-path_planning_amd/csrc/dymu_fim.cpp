@@ -104,6 +104,7 @@ struct dymu_ctx {
     uint64_t launches = 0;
     uint64_t max_passes = 0;
     int blocks = 0;
+    bool rehist = false;  // rebuild each list's histogram from its final keys
     uint32_t* lists[3] = {nullptr, nullptr, nullptr};
     uint32_t* counts[3] = {nullptr, nullptr, nullptr};
     size_t prof_used = 0;
@@ -223,6 +224,7 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
     variant = t8 >= c->prio_min_tiles ? 5 : 3;
   }
   if (need_keys && !is_prio(variant)) variant = 4;
+  if (c->opts.deterministic) variant = 5;
   const int TWd = tile_w(variant), THd = tile_h(variant);
   if (ghost_hi && (nrows % (uint32_t)THd) != 0) return DYMU_ERR_ARG;
   if (gj >= 0 && (gi < 0 || gi >= (int64_t)nx || gj >= (int64_t)nrows)) return DYMU_ERR_ARG;
@@ -260,15 +262,25 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
                              3ull * kShards * kBins, c->d_prio,
                              reinterpret_cast<double*>(c->d_prio + 3), prio_delta(c), c->prio_kappa,
                              st));
-    // default per pass: 64 8x8 tiles per CU (v4) / 8 16x16 tiles per CU (v5), the
-    // measured optima at 8192^2..16384^2; 4 per CU for whole grids below 2^17 16x16
-    // tiles (4096^2: 6.28 vs 6.50 ms, v11) and 10 per CU for whole grids from 2^20
-    // (16384^2: 35.8 vs 36.9 ms, v18, profiles/r02/sweep_v18b.log)
+    // kernel 5 relaxes one colour of a checkerboard of tiles per pass (PassArgs::checker):
+    // no visit then reads a halo another wave is writing, which cuts the tile visits
+    // by a third (16384^2: 36.8 -> 33.8 ms, 4096^2: 5.98 -> 5.48 ms, v23,
+    // profiles/r02/checker_sweep.txt).  DYMU_CHECKER=0 disables it.
+    bool checker = D.variant == 5;
+    if (const char* kv = std::getenv("DYMU_CHECKER")) checker = D.variant == 5 && std::atoi(kv);
+    if (c->opts.deterministic) checker = true;
+    // default per pass: 64 8x8 tiles per CU (v4) / 16x16 tiles per CU (v5), the measured
+    // optima: with the checkerboard 6 / 10 / 12 per CU for whole grids below 2^17 /
+    // below 2^20 / from 2^20 tiles (4096^2 / 8192^2 / 16384^2), 10 for slabs (8 without:
+    // same pass time in the rehearsal, 6% fewer exchange rounds); without it 4 / 8 / 10
+    // (v11, v18: profiles/r02/sweep_v18b.log)
     const bool whole5 = D.variant == 5 && !ghost_lo && !ghost_hi;
-    const uint32_t per_cu = D.variant != 5 ? 64u
-                            : (whole5 && ntiles < (1u << 17)) ? 4u
-                            : (whole5 && ntiles >= (1u << 20)) ? 10u
-                                                               : 8u;
+    const uint32_t per_cu = D.variant != 5                            ? 64u
+                            : !whole5                                  ? (checker ? 10u : 8u)
+                            : ntiles < (1u << 17)                      ? (checker ? 6u : 4u)
+                            : ntiles >= (1u << 20)                     ? (checker ? 12u : 10u)
+                                                                       : (checker ? 10u : 8u);
+    a.checker = checker;
     a.target = c->prio_target ? c->prio_target : (uint32_t)c->cu_count * per_cu;
     a.target_frac = c->prio_frac;
     a.prune = c->prune;
@@ -305,6 +317,10 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
     a.sweep_deadline = (uint32_t)std::max(0, std::atoi(kv));
   a.exact_sqrt = c->opts.exact_sqrt != 0;
   if (const char* kv = std::getenv("DYMU_EXACT_SQRT")) a.exact_sqrt = std::atoi(kv) != 0;
+  if (c->opts.deterministic) {
+    a.sweep_deadline = 0;  // the deadline makes the schedule timing-dependent
+    D.rehist = true;       // and so do the first-insertion keys of the histogram
+  }
   a.shard_cap = ntiles;
   a.tile_epoch = c->d_tile_epoch;
   a.stats = c->d_stats;
@@ -334,6 +350,7 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st, uint32_t report_seq = 0)
     a.count_out = D.counts[(p + 1) % 3];
     a.count_clear = D.counts[(p + 2) % 3];
     a.epoch = D.eb + (uint32_t)p + 2u;
+    a.checker_parity = (uint32_t)(p & 1u);
     if (is_prio(D.variant)) {
       a.key_in = prio_keys(c, p % 3);
       a.key_out = prio_keys(c, (p + 1) % 3);
@@ -363,6 +380,9 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st, uint32_t report_seq = 0)
       HIPC(c, hipMemsetAsync(c->d_trace, 0, sizeof(unsigned long long) * kTracePts * D.blocks, st));
       a.trace = c->d_trace;
     }
+    if (D.rehist)  // deterministic mode: b* from the list's final keys
+      HIPC(c, launch_rehist(a.list_in, a.count_in, a.shard_cap, a.key_in,
+                            const_cast<uint32_t*>(a.hist_in), a.base_in, a.delta, st));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (prof && D.launches % (uint64_t)c->profiling == 0) {
       while (c->prof_ev.size() < D.prof_used + 2) {
@@ -476,7 +496,9 @@ int dom_exchange(dymu_ctx* c, const double* lo, const double* hi, int32_t* d_tot
 // rank is the fixed point: nothing was queued after the previous round, and the
 // rows it produced improved no ghost.
 bool dom_round_ok(const dymu_ctx* c, uint64_t K) {
-  return c->dom.live && c->dom.variant == 5 && K >= 2;
+  // not in deterministic mode: the in-pass merge writes ghost rows that the same
+  // pass's boundary visits may be reading
+  return c->dom.live && c->dom.variant == 5 && K >= 2 && !c->opts.deterministic;
 }
 
 int dom_round(dymu_ctx* c, uint64_t K, const double* lo, const double* hi, int32_t* d_total,
@@ -877,6 +899,7 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
   if (const char* kv = std::getenv("DYMU_FIRST_BATCH"))
     c->first_batch = (uint64_t)std::max(1, std::atoi(kv));
   if (const char* kv = std::getenv("DYMU_PIPELINE")) c->pipeline = std::atoi(kv);
+  if (const char* kv = std::getenv("DYMU_DETERMINISTIC")) c->opts.deterministic = std::atoi(kv);
   if (const char* kv = std::getenv("DYMU_MAX_BATCH"))
     c->max_batch = (uint64_t)std::min(64, std::max(1, std::atoi(kv)));
   if (e == hipSuccess) {

@@ -59,6 +59,8 @@ struct PassArgs {
   unsigned long long* trace;  // debug: kTracePts s_memrealtime stamps per block, or null
   uint32_t sweep_deadline;  // kernel 5 (dyn): > 0: a visit stops sweeping this many 10-ns ticks
                             // after its workgroup started the pass (re-queued as if capped)
+  int checker;              // kernel 5: relax only tiles with (tx + ty + checker_parity) even
+  uint32_t checker_parity;  // (deterministic mode: no tile reads a halo being written)
   int exact_sqrt;  // kernel 5 (dyn): 1 = correctly rounded sweep sqrt (10 VALU), 0 = one
                    // Goldschmidt step (5 VALU, <= 36 ulp)
   // convergence mailbox: when set, block 0 stores (report_seq << 32) | n_active -- the
@@ -112,6 +114,12 @@ hipError_t launch_exchange(double* T, int64_t ld, int64_t nx, int64_t nrows, con
 hipError_t launch_eikonal_batch(const double* tx, const double* ty, const double* c, double* out,
                                 uint64_t n, int fast, hipStream_t st);
 hipError_t launch_sum_counts(const uint32_t* counts, int32_t* out, hipStream_t st);
+// deterministic mode: rebuild the key histogram of a list from its FINAL keys (the
+// enqueue path bins a tile by the key of its first insertion, which depends on the
+// order of the insertions); one workgroup, result in shard 0's row
+hipError_t launch_rehist(const uint32_t* list, const uint32_t* counts, uint32_t cap,
+                         const unsigned long long* keys, uint32_t* hist, const double* base,
+                         const double* delta, hipStream_t st);
 // computeCostMap state (SoA planner node fields, row-major pitch ld)
 struct CostState {
   double* cost;

@@ -1192,7 +1192,11 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     bool capped = false;
     const int sweeps = visit16<APPROX>(
         a, img, ek, true, tx, ty, lane, capped,
-        [&] { return key_bin(bitsd(kb), origin_in, inv_delta) <= bstar; }, stop_at);
+        [&] {
+          return key_bin(bitsd(kb), origin_in, inv_delta) <= bstar &&
+                 (!a.checker || ((uint32_t)(tx + ty) + a.checker_parity) % 2u == 0u);
+        },
+        stop_at);
     if (lane == 0) a.key_in[tile] = kInfBits;
     if (sweeps < 0) {  // deferred to the next pass with its key
       if (lane == 0) enqueue(tile, kb);
@@ -1631,6 +1635,43 @@ hipError_t launch_exchange(double* T, int64_t ld, int64_t nx, int64_t nrows, con
   const MergeArgs g{T,    ld,    nx,         nrows, ntx,  nty,    tile_w, list,  counts,
                     cap,  tile_epoch, epoch, keys,  hist, minkey, base,   delta};
   hipLaunchKernelGGL(k_exchange, dim3(blocks), dim3(256), 0, st, g, new_lo, new_hi, ticket, total);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(1024) void k_rehist(const uint32_t* list, const uint32_t* counts,
+                                                 uint32_t cap, const unsigned long long* keys,
+                                                 uint32_t* hist, const double* base,
+                                                 const double* delta) {
+  __shared__ uint32_t s_h[kBins];
+  __shared__ uint32_t s_pref[kShards + 1];
+  const int tid = threadIdx.x;
+  if (tid < kBins) s_h[tid] = 0u;
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int q = 0; q < kShards; ++q) {
+      s_pref[q] = acc;
+      acc += counts[q];
+    }
+    s_pref[kShards] = acc;
+  }
+  __syncthreads();
+  const double origin = *base, inv = 1.0 / *delta;
+  const uint32_t n = s_pref[kShards];
+  for (uint32_t e = tid; e < n; e += blockDim.x) {
+    int q = 0;
+    while (e >= s_pref[q + 1]) ++q;
+    const uint32_t t = list[(uint64_t)q * cap + (e - s_pref[q])];
+    atomicAdd(&s_h[key_bin(bitsd(keys[t]), origin, inv)], 1u);
+  }
+  __syncthreads();
+  for (int k = tid; k < kShards * kBins; k += blockDim.x) hist[k] = k < kBins ? s_h[k] : 0u;
+}
+
+hipError_t launch_rehist(const uint32_t* list, const uint32_t* counts, uint32_t cap,
+                         const unsigned long long* keys, uint32_t* hist, const double* base,
+                         const double* delta, hipStream_t st) {
+  hipLaunchKernelGGL(k_rehist, dim3(1), dim3(1024), 0, st, list, counts, cap, keys, hist, base,
+                     delta);
   return hipGetLastError();
 }
 

@@ -52,6 +52,7 @@ class DymuOpts(ctypes.Structure):
         ("kernel", ctypes.c_int),
         ("prio_target", ctypes.c_int),
         ("exact_sqrt", ctypes.c_int),
+        ("deterministic", ctypes.c_int),
     ]
 
 
@@ -203,11 +204,11 @@ class Engine:
 
     def __init__(self, device: int = -1, passes_per_check: int = 0, max_passes: int = 0,
                  max_inner: int = 0, grid_blocks: int = 0, kernel: int = 0,
-                 prio_target: int = 0, exact_sqrt: int = 0):
+                 prio_target: int = 0, exact_sqrt: int = 0, deterministic: int = 0):
         lib = load_fim()
         self._lib = lib
         opts = DymuOpts(device, passes_per_check, max_passes, max_inner, grid_blocks, kernel,
-                        prio_target, exact_sqrt)
+                        prio_target, exact_sqrt, deterministic)
         ctx = _vp()
         rc = lib.dymu_create(ctypes.byref(ctx), ctypes.byref(opts))
         if rc != DYMU_OK:

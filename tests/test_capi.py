@@ -59,7 +59,7 @@ def test_dist_rejects_bad_arguments(dymu):
 
 def test_abi_version_and_strerror(dymu):
     lib = dymu.load_fim()
-    assert lib.dymu_abi_version() == 4
+    assert lib.dymu_abi_version() == 5
     assert lib.dymu_strerror(-4) == b"pass cap reached before convergence"
 
 

@@ -315,3 +315,49 @@ def test_early_exit_modes(dymu, oracle, monkeypatch, mode):
         eng.free(dF)
         eng.free(dT)
         eng.close()
+
+
+def test_deterministic_mode_bit_reproducible(dymu, oracle):
+    """dymu_opts.deterministic: checkerboard passes, no sweep deadline -- two
+    contexts and two solves each give bit-identical maps, within the tolerance of
+    the oracle; the default schedule reaches the same fixed point."""
+    nx, ny, g = 1024, 768, (300, 500)
+    F = oracle.synth_speed(nx, ny, seed=21, obst_frac=0.03, obst_seed=22, goal=g)
+    maps, stats = [], []
+    for _ in range(2):
+        eng = dymu.Engine(deterministic=1, prio_target=64)
+        try:
+            for _ in range(2):
+                r = eng.solve(F, g[0], g[1])
+                maps.append(r.T)
+                stats.append(r.stats)
+        finally:
+            eng.close()
+    for T in maps[1:]:
+        assert np.array_equal(T.view(np.uint64), maps[0].view(np.uint64))
+    assert all(st["kernel"] == 5 for st in stats)
+    assert len({(st["passes"], st["tile_visits"], st["inner_sweeps"]) for st in stats}) == 1
+    Tref, _ = oracle.fmm(F, g)
+    assert_parity(maps[0], Tref)
+
+
+def test_deterministic_mode_large_grid(dymu):
+    """At 8192^2 the default run uses the sweep deadline; deterministic mode drops
+    it and repeats bit for bit (device-resident solve)."""
+    N, g = 8192, (4096, 4096)
+    eng = dymu.Engine(deterministic=1)
+    dF, dT = eng.alloc(8 * N * N), eng.alloc(8 * N * N)
+    try:
+        eng.synth_speed(dF, N, N, N, 0, 1, 0.02, 3, g[0], g[1])
+        outs = []
+        for _ in range(2):
+            st = eng.solve_device(dF, dT, N, N, N, g[0], g[1])
+            T = np.empty((N, N))
+            eng.d2h(T, dT)
+            outs.append((T, st))
+        assert np.array_equal(outs[0][0].view(np.uint64), outs[1][0].view(np.uint64))
+        assert outs[0][1]["passes"] == outs[1][1]["passes"]
+    finally:
+        eng.free(dF)
+        eng.free(dT)
+        eng.close()
