@@ -1184,19 +1184,25 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     if (e >= c1) break;
     const uint32_t tile =
         __builtin_amdgcn_readfirstlane(list_at_wave(a.list_in, a.shard_cap, s_pref, e, lane));
-    const unsigned long long kb = a.key_in[tile];
     const int tx = (int)(tile % (uint32_t)a.ntx);
     const int ty = (int)(tile / (uint32_t)a.ntx);
+    if (a.checker && ((uint32_t)(tx + ty) + a.checker_parity) % 2u != 0u) {
+      // the other colour of the checkerboard: deferred with its key, tile not loaded
+      if (lane == 0) {
+        const unsigned long long k0 = a.key_in[tile];
+        a.key_in[tile] = kInfBits;
+        enqueue(tile, k0);
+      }
+      ++my_defer;
+      continue;
+    }
+    const unsigned long long kb = a.key_in[tile];
     if (lane < 4) ek[lane] = kInfBits;
     if (trace && tid == 0 && first) trace[6] = __builtin_amdgcn_s_memrealtime();
     bool capped = false;
     const int sweeps = visit16<APPROX>(
         a, img, ek, true, tx, ty, lane, capped,
-        [&] {
-          return key_bin(bitsd(kb), origin_in, inv_delta) <= bstar &&
-                 (!a.checker || ((uint32_t)(tx + ty) + a.checker_parity) % 2u == 0u);
-        },
-        stop_at);
+        [&] { return key_bin(bitsd(kb), origin_in, inv_delta) <= bstar; }, stop_at);
     if (lane == 0) a.key_in[tile] = kInfBits;
     if (sweeps < 0) {  // deferred to the next pass with its key
       if (lane == 0) enqueue(tile, kb);
