@@ -270,7 +270,7 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
     if (const char* kv = std::getenv("DYMU_CHECKER")) checker = D.variant == 5 && std::atoi(kv);
     if (c->opts.deterministic) checker = true;
     // default per pass: 64 8x8 tiles per CU (v4) / 16x16 tiles per CU (v5), the measured
-    // optima: with the checkerboard 6 / 10 / 12 per CU for whole grids below 2^17 /
+    // optima: with the checkerboard 6 / 12 / 14 per CU for whole grids below 2^17 /
     // below 2^20 / from 2^20 tiles (4096^2 / 8192^2 / 16384^2), 10 for slabs (8 without:
     // same pass time in the rehearsal, 6% fewer exchange rounds); without it 4 / 8 / 10
     // (v11, v18: profiles/r02/sweep_v18b.log)
@@ -278,8 +278,8 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
     const uint32_t per_cu = D.variant != 5                            ? 64u
                             : !whole5                                  ? (checker ? 10u : 8u)
                             : ntiles < (1u << 17)                      ? (checker ? 6u : 4u)
-                            : ntiles >= (1u << 20)                     ? (checker ? 12u : 10u)
-                                                                       : (checker ? 10u : 8u);
+                            : ntiles >= (1u << 20)                     ? (checker ? 14u : 10u)
+                                                                       : (checker ? 12u : 8u);
     a.checker = checker;
     a.target = c->prio_target ? c->prio_target : (uint32_t)c->cu_count * per_cu;
     a.target_frac = c->prio_frac;
