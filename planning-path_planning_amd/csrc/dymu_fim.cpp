@@ -153,7 +153,8 @@ int ensure_tiles(dymu_ctx* c, uint32_t ntiles, hipStream_t st) {
 }
 
 int ensure_prio(dymu_ctx* c, uint32_t ntiles) {
-  if (!c->d_hist) HIPC(c, hipMalloc(&c->d_hist, sizeof(uint32_t) * 3 * kShards * kBins));
+  // 3 list histograms + 2 rebuild buffers (deterministic mode)
+  if (!c->d_hist) HIPC(c, hipMalloc(&c->d_hist, sizeof(uint32_t) * 5 * kShards * kBins));
   if (!c->d_prio) HIPC(c, hipMalloc(&c->d_prio, sizeof(unsigned long long) * 8));
   if (ntiles <= c->keys_cap) return DYMU_OK;
   if (c->d_keys) (void)hipFree(c->d_keys);
@@ -320,6 +321,8 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   if (c->opts.deterministic) {
     a.sweep_deadline = 0;  // the deadline makes the schedule timing-dependent
     D.rehist = true;       // and so do the first-insertion keys of the histogram
+    HIPC(c, hipMemsetAsync(c->d_hist + (uint64_t)3 * kShards * kBins, 0,
+                           sizeof(uint32_t) * 2 * kShards * kBins, st));
   }
   a.shard_cap = ntiles;
   a.tile_epoch = c->d_tile_epoch;
@@ -380,9 +383,14 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st, uint32_t report_seq = 0)
       HIPC(c, hipMemsetAsync(c->d_trace, 0, sizeof(unsigned long long) * kTracePts * D.blocks, st));
       a.trace = c->d_trace;
     }
-    if (D.rehist)  // deterministic mode: b* from the list's final keys
-      HIPC(c, launch_rehist(a.list_in, a.count_in, a.shard_cap, a.key_in,
-                            const_cast<uint32_t*>(a.hist_in), a.base_in, a.delta, st));
+    if (D.rehist) {  // deterministic mode: b* from the list's final keys
+      uint32_t* rh = c->d_hist + (uint64_t)3 * kShards * kBins;  // 2 alternating buffers
+      uint32_t* mine = rh + (p & 1u) * kShards * kBins;
+      uint32_t* next = rh + ((p + 1) & 1u) * kShards * kBins;
+      HIPC(c, launch_rehist(a.list_in, a.count_in, a.shard_cap, a.key_in, a.base_in, a.delta,
+                            mine, next, st));
+      a.hist_in = mine;
+    }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (prof && D.launches % (uint64_t)c->profiling == 0) {
       while (c->prof_ev.size() < D.prof_used + 2) {

@@ -116,10 +116,11 @@ hipError_t launch_eikonal_batch(const double* tx, const double* ty, const double
 hipError_t launch_sum_counts(const uint32_t* counts, int32_t* out, hipStream_t st);
 // deterministic mode: rebuild the key histogram of a list from its FINAL keys (the
 // enqueue path bins a tile by the key of its first insertion, which depends on the
-// order of the insertions); one workgroup, result in shard 0's row
+// order of the insertions) into shard 0's row of `out`; `zero` (the other of two
+// alternating buffers) is cleared for the next rebuild
 hipError_t launch_rehist(const uint32_t* list, const uint32_t* counts, uint32_t cap,
-                         const unsigned long long* keys, uint32_t* hist, const double* base,
-                         const double* delta, hipStream_t st);
+                         const unsigned long long* keys, const double* base, const double* delta,
+                         uint32_t* out, uint32_t* zero, hipStream_t st);
 // computeCostMap state (SoA planner node fields, row-major pitch ld)
 struct CostState {
   double* cost;

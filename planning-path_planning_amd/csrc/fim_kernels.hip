@@ -1644,40 +1644,35 @@ hipError_t launch_exchange(double* T, int64_t ld, int64_t nx, int64_t nrows, con
   return hipGetLastError();
 }
 
-__global__ __launch_bounds__(1024) void k_rehist(const uint32_t* list, const uint32_t* counts,
-                                                 uint32_t cap, const unsigned long long* keys,
-                                                 uint32_t* hist, const double* base,
-                                                 const double* delta) {
+// Deterministic mode: rebuild list p's key histogram from its FINAL keys into
+// shard 0's row of `out` (zeroed by the previous pass's rebuild); block (0,0)
+// zeroes `zero`, the buffer the next rebuild fills.  Blocks (x, q) take shard q.
+__global__ __launch_bounds__(256) void k_rehist(const uint32_t* list, const uint32_t* counts,
+                                                uint32_t cap, const unsigned long long* keys,
+                                                const double* base, const double* delta,
+                                                uint32_t* out, uint32_t* zero) {
   __shared__ uint32_t s_h[kBins];
-  __shared__ uint32_t s_pref[kShards + 1];
   const int tid = threadIdx.x;
+  const uint32_t q = blockIdx.y;
   if (tid < kBins) s_h[tid] = 0u;
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (int q = 0; q < kShards; ++q) {
-      s_pref[q] = acc;
-      acc += counts[q];
-    }
-    s_pref[kShards] = acc;
-  }
+  if (blockIdx.x == 0 && q == 0)
+    for (int k = tid; k < kShards * kBins; k += blockDim.x) zero[k] = 0u;
   __syncthreads();
+  const uint32_t n = counts[q];
   const double origin = *base, inv = 1.0 / *delta;
-  const uint32_t n = s_pref[kShards];
-  for (uint32_t e = tid; e < n; e += blockDim.x) {
-    int q = 0;
-    while (e >= s_pref[q + 1]) ++q;
-    const uint32_t t = list[(uint64_t)q * cap + (e - s_pref[q])];
+  for (uint32_t i = blockIdx.x * blockDim.x + tid; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t t = list[(uint64_t)q * cap + i];
     atomicAdd(&s_h[key_bin(bitsd(keys[t]), origin, inv)], 1u);
   }
   __syncthreads();
-  for (int k = tid; k < kShards * kBins; k += blockDim.x) hist[k] = k < kBins ? s_h[k] : 0u;
+  if (tid < kBins && s_h[tid]) atomicAdd(&out[tid], s_h[tid]);
 }
 
 hipError_t launch_rehist(const uint32_t* list, const uint32_t* counts, uint32_t cap,
-                         const unsigned long long* keys, uint32_t* hist, const double* base,
-                         const double* delta, hipStream_t st) {
-  hipLaunchKernelGGL(k_rehist, dim3(1), dim3(1024), 0, st, list, counts, cap, keys, hist, base,
-                     delta);
+                         const unsigned long long* keys, const double* base, const double* delta,
+                         uint32_t* out, uint32_t* zero, hipStream_t st) {
+  hipLaunchKernelGGL(k_rehist, dim3(8, kShards), dim3(256), 0, st, list, counts, cap, keys, base,
+                     delta, out, zero);
   return hipGetLastError();
 }
 
