@@ -361,3 +361,20 @@ def test_deterministic_mode_large_grid(dymu):
         eng.free(dF)
         eng.free(dT)
         eng.close()
+
+
+@pytest.mark.parametrize("checker", ["0", "1"])
+def test_checkerboard_on_off(dymu, oracle, monkeypatch, checker):
+    """Kernel 5 with and without checkerboard passes (DYMU_CHECKER) reaches the
+    oracle's fixed point; the checkerboard relaxes fewer tiles."""
+    monkeypatch.setenv("DYMU_CHECKER", checker)
+    nx, ny, g = 768, 640, (200, 300)
+    F = oracle.synth_speed(nx, ny, seed=31, obst_frac=0.03, obst_seed=32, goal=g)
+    eng = dymu.Engine(kernel=5, prio_target=64)
+    try:
+        r = eng.solve(F, g[0], g[1])
+    finally:
+        eng.close()
+    Tref, _ = oracle.fmm(F, g)
+    assert_parity(r.T, Tref)
+    assert r.stats["kernel"] == 5 and r.stats["tile_visits"] > 0
