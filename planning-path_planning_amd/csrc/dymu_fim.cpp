@@ -33,10 +33,13 @@ struct dymu_ctx {
 
   // 3: two 8x8 tiles per wave (red-black), 4: v3 body + priority passes;
   // 5: priority passes on 16x16 tiles (one per wave, 16-wave workgroups);
-  // 0 (default): per domain, 5 from prio_min_tiles 8x8 tiles up, else 3.
+  // 0 (default): per domain, 5 from prio_min_tiles 8x8 tiles up, else 3.  Since the
+  // checkerboard passes (v23) kernel 5 is the faster one at every size measured (256^2:
+  // 0.45 vs 0.51 ms, 1024^2: 1.22 vs 1.63, 2048^2: 2.4-2.9 vs 4.1-4.3, 2896^2: 3.52 vs
+  // 6.60; profiles/r02/small_grids.txt), so the threshold is 0.
   // DYMU_KERNEL overrides
   int variant = 0;
-  uint32_t prio_min_tiles = 1u << 17;  // DYMU_PRIO_MIN_TILES (~2900^2 cells)
+  uint32_t prio_min_tiles = 0;  // DYMU_PRIO_MIN_TILES
   uint32_t prio_target = 0;  // v4/v5: tiles relaxed per pass; 0 = per-variant default
   double prio_kappa = 0.5;   // v4: histogram bin width / mean F (DYMU_PRIO_KAPPA)
   float prio_frac = 0.0f;    // v4: ... or this fraction of the active list (DYMU_PRIO_FRAC)

@@ -63,17 +63,27 @@ def test_parity_random(kengine, oracle, nx, ny, frac, goal):
     assert r.T[goal[1], goal[0]] == 0.0
 
 
-def test_constant_speed_closed_form(engine):
-    """C=1: T on the axes equals the distance, T(+-1,+-1) = 1 + sqrt(2)/2 (:533)."""
+@pytest.mark.parametrize("exact", [1, 0])
+def test_constant_speed_closed_form(dymu, exact):
+    """C=1: T on the axes equals the distance, T(+-1,+-1) = 1 + sqrt(2)/2 (:533) --
+    bit for bit with the correctly rounded sweep sqrt (exact_sqrt=1), within the
+    default candidate's 36-ulp bound otherwise."""
     N = 65
     F = np.ones((N, N))
-    r = engine.solve(F, 32, 32)
+    eng = dymu.Engine(exact_sqrt=exact)
+    try:
+        r = eng.solve(F, 32, 32)
+    finally:
+        eng.close()
     T = r.T
     for k in range(1, 20):
         assert T[32, 32 + k] == float(k) and T[32 - k, 32] == float(k)
     v = 1.0 + np.sqrt(2.0) / 2.0
     for dj, di in ((1, 1), (-1, 1), (1, -1), (-1, -1)):
-        assert T[32 + dj, 32 + di] == v
+        if exact:
+            assert T[32 + dj, 32 + di] == v
+        else:
+            assert abs(T[32 + dj, 32 + di] - v) <= 36 * np.spacing(v)
 
 
 def test_device_resident_and_synth(engine, oracle):
@@ -131,12 +141,12 @@ def test_priority_kernel_defers(dymu, oracle):
 
 
 def test_auto_kernel_choice(dymu):
-    """kernel=0 picks plain FIM below 2^17 8x8 tiles (~2900^2 cells) and
-    16x16 priority passes from there up."""
+    """kernel=0 picks the 16x16 priority passes at every size (the checkerboard
+    made them the faster kernel down to 256^2); kernel=3 still selects plain FIM."""
     eng = dymu.Engine()
     try:
         r = eng.solve(np.ones((64, 64)), 3, 3)
-        assert r.stats["kernel"] == 3 and r.stats["tile_w"] == 8
+        assert r.stats["kernel"] == 5 and r.stats["tile_w"] == 16
         r = eng.solve(np.ones((2900, 2900)), 3, 3)
         assert r.stats["kernel"] == 5 and r.stats["tile_w"] == 16
         assert r.T[3, 13] == 10.0  # on the axis through the goal: the distance
@@ -378,3 +388,16 @@ def test_checkerboard_on_off(dymu, oracle, monkeypatch, checker):
     Tref, _ = oracle.fmm(F, g)
     assert_parity(r.T, Tref)
     assert r.stats["kernel"] == 5 and r.stats["tile_visits"] > 0
+
+
+def test_plain_fim_kernel_still_selectable(dymu, oracle):
+    """dymu_opts.kernel = 3 (plain block FIM, 8x8 tiles) remains a parity-green choice."""
+    F = oracle.synth_speed(300, 200, seed=41, obst_frac=0.03, obst_seed=42, goal=(20, 150))
+    eng = dymu.Engine(kernel=3)
+    try:
+        r = eng.solve(F, 20, 150)
+    finally:
+        eng.close()
+    assert r.stats["kernel"] == 3 and r.stats["tile_w"] == 8
+    Tref, _ = oracle.fmm(F, (20, 150))
+    assert_parity(r.T, Tref)
