@@ -166,6 +166,9 @@ class DyMuPathPlanner {
   // Flat row-major views for FFI callers (ny*nx, index j*nx + i).  The total
   // cost lives on the device; this downloads whatever the host copy lacks.
   const double* totalCostData() const;
+  // The whole total cost into out (ny*nx): raw (+inf unreachable) or as
+  // getTotalCostMatrix (-1), row ranges on the host threads.
+  void copyTotalCost(double* out, bool raw) const;
   unsigned sizeX() const { return nx_; }
   unsigned sizeY() const { return ny_; }
   bool hasGoal() const { return has_goal_; }

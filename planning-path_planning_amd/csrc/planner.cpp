@@ -543,6 +543,22 @@ const double* DyMuPathPlanner::totalCostData() const {
   return total_cost_.data();
 }
 
+// One pass over the host mirror split in row ranges: at 16384^2 a single-thread
+// copy into a caller's fresh buffer (first-touch faults on 2 GiB) costs several
+// times the solve itself.
+void DyMuPathPlanner::copyTotalCost(double* out, bool raw) const {
+  fetchAll();
+  const double* t = total_cost_.data();
+  parallel_rows(ny_, [&](unsigned j0, unsigned j1) {
+    const uint64_t a = idx(0, j0), b = idx(0, j1);
+    if (raw) {
+      std::memcpy(out + a, t + a, sizeof(double) * (b - a));
+    } else {
+      for (uint64_t k = a; k < b; ++k) out[k] = t[k] == kInf ? -1.0 : t[k];
+    }
+  });
+}
+
 bool DyMuPathPlanner::closedCell(uint64_t k) const {
   const double t = T(k);
   return t < kInf && t <= closed_limit_;
@@ -873,12 +889,15 @@ std::string DyMuPathPlanner::getLocomotionMode(base::Waypoint wPos) {
 // :799-811
 std::vector<std::vector<double>> DyMuPathPlanner::getTotalCostMatrix() {
   fetchAll();
-  std::vector<std::vector<double>> m(ny_, std::vector<double>(nx_));
-  for (unsigned j = 0; j < ny_; ++j)
-    for (unsigned i = 0; i < nx_; ++i) {
-      const double t = total_cost_[idx(i, j)];
-      m[j][i] = (t == kInf) ? -1.0 : t;
+  std::vector<std::vector<double>> m(ny_);
+  parallel_rows(ny_, [&](unsigned j0, unsigned j1) {
+    for (unsigned j = j0; j < j1; ++j) {
+      const double* t = &total_cost_[idx(0, j)];
+      std::vector<double>& r = m[j];
+      r.resize(nx_);
+      for (unsigned i = 0; i < nx_; ++i) r[i] = (t[i] == kInf) ? -1.0 : t[i];
     }
+  });
   return m;
 }
 

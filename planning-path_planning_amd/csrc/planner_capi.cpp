@@ -126,7 +126,7 @@ int dymu_planner_compute_entire_total_cost_map(dymu_planner* p) {
 
 int dymu_planner_get_total_cost_matrix(dymu_planner* p, double* out) {
   if (!p || !out) return DYMU_ERR_ARG;
-  return guarded([&] { from_rows(p->pl.getTotalCostMatrix(), out); return DYMU_OK; });
+  return guarded([&] { p->pl.copyTotalCost(out, false); return DYMU_OK; });
 }
 
 int dymu_planner_get_global_cost_matrix(dymu_planner* p, double* out) {
@@ -146,9 +146,7 @@ int dymu_planner_get_trafficability_matrix(dymu_planner* p, double* out) {
 
 int dymu_planner_get_total_cost_raw(dymu_planner* p, double* out) {
   if (!p || !out) return DYMU_ERR_ARG;
-  const size_t n = (size_t)p->pl.sizeX() * p->pl.sizeY();
-  std::memcpy(out, p->pl.totalCostData(), sizeof(double) * n);
-  return DYMU_OK;
+  return guarded([&] { p->pl.copyTotalCost(out, true); return DYMU_OK; });
 }
 
 int dymu_planner_get_total_cost(dymu_planner* p, double x, double y, double z, double h,
