@@ -383,3 +383,35 @@ def test_terrain_class_beyond_lut_is_obstacle(dymu, oracle):
     mask = np.ones((N, N), bool)
     mask[9:15, 9:15] = False  # the block and the ring its raw cost is smoothed into
     assert np.array_equal(G[mask], ref[mask])
+
+
+@pytest.mark.gpu
+def test_total_cost_readbacks_chunked(dymu, oracle):
+    """copyTotalCost's chunked download (a stale mirror with >= 1024 rows goes down in
+    16 row chunks, each copied out while the next downloads): raw and -1 forms, both
+    orders, ragged last chunk, and blocks already fetched by a point query."""
+    nx, ny, goal = 640, 1100, (300, 700)
+    F = oracle.synth_speed(nx, ny, seed=12, obst_frac=0.03, obst_seed=13, goal=goal)
+    Tref, _ = oracle.fmm(F, goal)
+    Mref = np.where(np.isinf(Tref), -1.0, Tref)
+    p = dymu.Planner()
+    assert p.initGlobalLayer(1.0, 0.5, nx, ny)
+    assert p.setCostMap(np.where(np.isfinite(F), F, -1.0))
+    for first_raw in (True, False):
+        assert p.setGoal(goal)
+        assert p.computeEntireTotalCostMap()
+        p.getTotalCost((17.0, 1050.0))  # one mirror block fetched on its own
+        a = p.totalCostRaw() if first_raw else p.getTotalCostMatrix()
+        b = p.getTotalCostMatrix() if first_raw else p.totalCostRaw()
+        T, M = (a, b) if first_raw else (b, a)
+        assert T.shape == (ny, nx) and M.shape == (ny, nx)
+        assert np.array_equal(np.isinf(T), np.isinf(Tref))
+        assert np.array_equal(M == -1.0, Mref == -1.0)
+        fin = np.isfinite(Tref)
+        assert (np.abs(T[fin] - Tref[fin]) / np.maximum(1, Tref[fin])).max() <= RTOL
+        assert np.array_equal(np.where(np.isinf(T), -1.0, T), M)
+        # a second solve with another goal leaves no stale rows behind
+        assert p.setGoal((goal[0] + 1, goal[1]))
+        assert p.computeEntireTotalCostMap()
+        T2 = p.totalCostRaw()
+        assert T2[goal[1], goal[0] + 1] == 0.0 and T2[goal[1], goal[0]] > 0.0
