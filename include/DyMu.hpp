@@ -212,6 +212,10 @@ class DyMuPathPlanner {
   // of kBlk x kBlk cells on first read
   double T(uint64_t k) const;
   void fetchAll() const;
+  // body(r0, r1) over row chunks of the total cost, each once it is in the host
+  // mirror (a stale mirror downloads chunk k+1 while body runs on chunk k)
+  template <class Body>
+  void streamTotalCost(Body&& body) const;
   // the reference's node state: CLOSED iff popped by its FMM (finite T not above
   // the last early-exit limit; every finite cell after a full solve)
   bool closedCell(uint64_t k) const;

@@ -546,11 +546,37 @@ const double* DyMuPathPlanner::totalCostData() const {
 // One pass over the host mirror split in row ranges: at 16384^2 a single-thread
 // copy into a caller's fresh buffer (first-touch faults on 2 GiB) costs several
 // times the solve itself.
-// A stale mirror is downloaded in row chunks and each chunk is copied out while
+// A stale mirror is downloaded in row chunks and each chunk is handed on while
 // the next one downloads.
+template <class Body>
+void DyMuPathPlanner::streamTotalCost(Body&& body) const {
+  constexpr unsigned kChunks = 16;
+  if (!blk_missing_ || ny_ < 64 * kChunks) {
+    fetchAll();
+    body(0u, ny_);
+    return;
+  }
+  const unsigned step = (ny_ + kChunks - 1) / kChunks;
+  std::thread worker;
+  std::string failed;
+  for (unsigned r0 = 0; r0 < ny_ && failed.empty(); r0 += step) {
+    const unsigned r1 = std::min(ny_, r0 + step);
+    const uint64_t o = idx(0, r0);
+    if (dymu_memcpy_d2h(ctx_, &total_cost_[o], dT_ + o, sizeof(double) * (idx(0, r1) - o)) !=
+        DYMU_OK)
+      failed = dymu_last_error(ctx_);
+    if (worker.joinable()) worker.join();
+    if (failed.empty()) worker = std::thread([&body, r0, r1] { body(r0, r1); });
+  }
+  if (worker.joinable()) worker.join();
+  if (!failed.empty()) throw std::runtime_error("dymu: total-cost download failed: " + failed);
+  std::fill(blk_ok_.begin(), blk_ok_.end(), 1);
+  blk_missing_ = 0;
+}
+
 void DyMuPathPlanner::copyTotalCost(double* out, bool raw) const {
   const double* t = total_cost_.data();
-  auto copy_rows = [&](unsigned r0, unsigned r1) {
+  streamTotalCost([&](unsigned r0, unsigned r1) {
     parallel_rows(r1 - r0, [&](unsigned j0, unsigned j1) {
       const uint64_t a = idx(0, r0 + j0), b = idx(0, r0 + j1);
       if (raw) {
@@ -559,29 +585,7 @@ void DyMuPathPlanner::copyTotalCost(double* out, bool raw) const {
         for (uint64_t k = a; k < b; ++k) out[k] = t[k] == kInf ? -1.0 : t[k];
       }
     });
-  };
-  constexpr unsigned kChunks = 16;
-  if (!blk_missing_ || ny_ < 64 * kChunks) {
-    fetchAll();
-    copy_rows(0, ny_);
-    return;
-  }
-  const unsigned step = (ny_ + kChunks - 1) / kChunks;
-  std::thread copier;
-  std::string failed;
-  for (unsigned r0 = 0; r0 < ny_ && failed.empty(); r0 += step) {
-    const unsigned r1 = std::min(ny_, r0 + step);
-    const uint64_t o = idx(0, r0);
-    if (dymu_memcpy_d2h(ctx_, &total_cost_[o], dT_ + o, sizeof(double) * (idx(0, r1) - o)) !=
-        DYMU_OK)
-      failed = dymu_last_error(ctx_);
-    if (copier.joinable()) copier.join();
-    if (failed.empty()) copier = std::thread(copy_rows, r0, r1);
-  }
-  if (copier.joinable()) copier.join();
-  if (!failed.empty()) throw std::runtime_error("dymu: total-cost download failed: " + failed);
-  std::fill(blk_ok_.begin(), blk_ok_.end(), 1);
-  blk_missing_ = 0;
+  });
 }
 
 bool DyMuPathPlanner::closedCell(uint64_t k) const {
@@ -913,15 +917,18 @@ std::string DyMuPathPlanner::getLocomotionMode(base::Waypoint wPos) {
 
 // :799-811
 std::vector<std::vector<double>> DyMuPathPlanner::getTotalCostMatrix() {
-  fetchAll();
   std::vector<std::vector<double>> m(ny_);
   parallel_rows(ny_, [&](unsigned j0, unsigned j1) {
-    for (unsigned j = j0; j < j1; ++j) {
-      const double* t = &total_cost_[idx(0, j)];
-      std::vector<double>& r = m[j];
-      r.resize(nx_);
-      for (unsigned i = 0; i < nx_; ++i) r[i] = (t[i] == kInf) ? -1.0 : t[i];
-    }
+    for (unsigned j = j0; j < j1; ++j) m[j].resize(nx_);
+  });
+  streamTotalCost([&](unsigned r0, unsigned r1) {
+    parallel_rows(r1 - r0, [&](unsigned j0, unsigned j1) {
+      for (unsigned j = r0 + j0; j < r0 + j1; ++j) {
+        const double* t = &total_cost_[idx(0, j)];
+        std::vector<double>& r = m[j];
+        for (unsigned i = 0; i < nx_; ++i) r[i] = (t[i] == kInf) ? -1.0 : t[i];
+      }
+    });
   });
   return m;
 }
