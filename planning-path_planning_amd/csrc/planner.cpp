@@ -61,6 +61,9 @@ DyMuPathPlanner::~DyMuPathPlanner() {
 
 void DyMuPathPlanner::setEngineOptions(const dymu_opts& o) {
   opts_ = o;
+  // the solved map lives in dT_: bring the host mirror up to date before the
+  // device buffers go, so T(), getPath and the matrix getters keep working
+  if (ctx_ && dT_ && blk_missing_) fetchAll();
   release_engine(ctx_, dF_, dT_, registered_, dcells_);
   solved_ = false;
   speed_valid_ = false;
@@ -153,6 +156,9 @@ unsigned host_threads() {
 // least 64 rows each).  Every loop run this way writes only the node it visits
 // and reads fields no iteration of the same loop writes, so the split changes no
 // value -- the results are those of the reference's single raster loop.
+// Exceptions thrown by body on a worker thread are carried back and rethrown on
+// the calling thread (a throw escaping a std::thread would std::terminate); the
+// started threads are joined on every path, a failed thread start included.
 template <class Body>
 void parallel_rows(unsigned ny, Body&& body) {
   const unsigned nt = std::max(1u, std::min(host_threads(), ny / 64));
@@ -160,15 +166,38 @@ void parallel_rows(unsigned ny, Body&& body) {
     body(0u, ny);
     return;
   }
-  std::vector<std::thread> pool;
-  pool.reserve(nt - 1);
   const unsigned step = (ny + nt - 1) / nt;
-  for (unsigned t = 1; t < nt; ++t) {
-    const unsigned j0 = t * step, j1 = std::min(ny, j0 + step);
-    if (j0 < j1) pool.emplace_back([&body, j0, j1] { body(j0, j1); });
+  std::vector<std::exception_ptr> errs(nt);
+  struct Joiner {
+    std::vector<std::thread> pool;
+    ~Joiner() {
+      for (auto& th : pool)
+        if (th.joinable()) th.join();
+    }
+  } J;
+  J.pool.reserve(nt - 1);
+  auto run = [&body, &errs](unsigned t, unsigned j0, unsigned j1) {
+    try {
+      body(j0, j1);
+    } catch (...) {
+      errs[t] = std::current_exception();
+    }
+  };
+  try {
+    for (unsigned t = 1; t < nt; ++t) {
+      const unsigned j0 = t * step, j1 = std::min(ny, j0 + step);
+      if (j0 < j1) J.pool.emplace_back(run, t, j0, j1);
+    }
+  } catch (...) {  // std::system_error from a thread start: finish what started, rethrow
+    for (auto& th : J.pool) th.join();
+    J.pool.clear();
+    throw;
   }
-  body(0u, std::min(ny, step));
-  for (auto& th : pool) th.join();
+  run(0u, 0u, std::min(ny, step));
+  for (auto& th : J.pool) th.join();
+  J.pool.clear();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
 }
 
 }  // namespace
@@ -557,19 +586,36 @@ void DyMuPathPlanner::streamTotalCost(Body&& body) const {
     return;
   }
   const unsigned step = (ny_ + kChunks - 1) / kChunks;
-  std::thread worker;
-  std::string failed;
-  for (unsigned r0 = 0; r0 < ny_ && failed.empty(); r0 += step) {
+  // the return code is the failure flag (some failures leave no error text)
+  int rc = DYMU_OK;
+  std::exception_ptr body_err;
+  struct Joiner {
+    std::thread th;
+    ~Joiner() {
+      if (th.joinable()) th.join();
+    }
+  } worker;
+  for (unsigned r0 = 0; r0 < ny_ && rc == DYMU_OK && !body_err; r0 += step) {
     const unsigned r1 = std::min(ny_, r0 + step);
     const uint64_t o = idx(0, r0);
-    if (dymu_memcpy_d2h(ctx_, &total_cost_[o], dT_ + o, sizeof(double) * (idx(0, r1) - o)) !=
-        DYMU_OK)
-      failed = dymu_last_error(ctx_);
-    if (worker.joinable()) worker.join();
-    if (failed.empty()) worker = std::thread([&body, r0, r1] { body(r0, r1); });
+    rc = dymu_memcpy_d2h(ctx_, &total_cost_[o], dT_ + o, sizeof(double) * (idx(0, r1) - o));
+    if (worker.th.joinable()) worker.th.join();
+    if (rc == DYMU_OK && !body_err)
+      worker.th = std::thread([&body, &body_err, r0, r1] {
+        try {
+          body(r0, r1);
+        } catch (...) {
+          body_err = std::current_exception();
+        }
+      });
   }
-  if (worker.joinable()) worker.join();
-  if (!failed.empty()) throw std::runtime_error("dymu: total-cost download failed: " + failed);
+  if (worker.th.joinable()) worker.th.join();
+  if (rc != DYMU_OK) {
+    const char* msg = ctx_ ? dymu_last_error(ctx_) : "";
+    throw std::runtime_error(std::string("dymu: total-cost download failed: ") +
+                             (msg && *msg ? msg : dymu_strerror(rc)));
+  }
+  if (body_err) std::rethrow_exception(body_err);
   std::fill(blk_ok_.begin(), blk_ok_.end(), 1);
   blk_missing_ = 0;
 }
@@ -730,6 +776,9 @@ void DyMuPathPlanner::replayBand(double t_closed, const std::vector<uint64_t>& b
       const auto key = std::make_pair(k, t);
       auto it = memo.find(key);
       if (it != memo.end()) return it->second;
+      // in progress: a tie cycle (two OPEN cells each reached through a CLOSED
+      // neighbour of exactly equal T) reads +inf here instead of recursing
+      memo.emplace(key, kInf);
       const int64_t i = (int64_t)(k % NX), j = (int64_t)(k / NX);
       double v = kInf;
       const int64_t nb[4][2] = {{i, j - 1}, {i - 1, j}, {i + 1, j}, {i, j + 1}};
@@ -740,7 +789,7 @@ void DyMuPathPlanner::replayBand(double t_closed, const std::vector<uint64_t>& b
         const double ty = axis(i, j - 1, i, j + 1, te, depth);
         v = std::fmin(v, eikonal(tx, ty, C));
       }
-      memo.emplace(key, v);
+      memo[key] = v;
       return v;
     }
   } rec{*this, speed_.data(), t_closed, (int64_t)nx_, (int64_t)ny_, {}};

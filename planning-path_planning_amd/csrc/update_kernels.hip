@@ -93,11 +93,13 @@ __global__ void k_reset_seed(UpdateArgs a) {
 }
 
 // Decrease-only change (every speed in W went down or stayed): the old map is a
-// valid upper bound of the new fixed point everywhere, and a cell whose value
-// changes has a new optimal path entering W from its ring, so its new value is
-// above min old T over the ring >= theta; no cell needs a reset.  Seed every tile
-// that intersects W (tiles [tx0,tx1) x [ty0,ty1)) with key theta; the passes
-// then lower whatever the cheaper window reaches.
+// valid upper bound of the new fixed point everywhere, so no cell needs a reset.
+// theta is a lower bound on every new value the passes can produce: with the goal
+// outside W, a cell whose value changes has a new optimal path that enters W from
+// its ring, so its new value is above min old T over the ring >= theta; with the
+// goal inside W (or its ring) theta = T(goal) = 0, trivially a lower bound.  Seed
+// every tile that intersects W (tiles [tx0,tx1) x [ty0,ty1)) with key theta; the
+// passes then lower whatever the cheaper window reaches.
 __global__ void k_seed_window(UpdateArgs a, uint32_t tx0, uint32_t ty0, uint32_t tx1,
                               uint32_t ty1) {
   const uint32_t w = tx1 - tx0, n = w * (ty1 - ty0);

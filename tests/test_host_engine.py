@@ -1,0 +1,70 @@
+"""The planner's host logic over a host-memory test double of the engine C-ABI
+(tests/hostengine/host_engine.c: malloc'd "device" buffers, the oracle's heap FMM
+as the solve), on CPU:
+  * a >= 1024-row readback (getTotalCostMatrix's chunked download) whose device
+    copy fails WITHOUT an error text must throw, not return stale rows;
+  * setEngineOptions after a solve keeps the solved map readable (map + path);
+  * computeTotalCostMap's early exit on a constant-cost map (every distance ties)
+    finishes with exact CLOSED values (the band replay's tie cycles).
+Never part of the product: the product links the HIP engine, which has no CPU path."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FLAGS = ["-O1", "-g", "-ffp-contract=off", "-pthread"]
+
+
+@pytest.fixture(scope="module")
+def driver(tmp_path_factory):
+    if shutil.which("g++") is None:
+        pytest.skip("needs gcc/g++")
+    d = tmp_path_factory.mktemp("hostengine")
+    inc = ["-I" + os.path.join(ROOT, p) for p in ("include", "oracle",
+                                                 "planning-path_planning_amd/csrc")]
+    objs = []
+    for src in ("oracle/oracle.c", "tests/hostengine/host_engine.c"):
+        o = str(d / (os.path.basename(src) + ".o"))
+        subprocess.run(["gcc", *FLAGS, "-std=gnu11", *inc, "-c", os.path.join(ROOT, src),
+                        "-o", o], check=True)
+        objs.append(o)
+    exe = str(d / "driver")
+    srcs = [os.path.join(ROOT, s) for s in (
+        "tests/hostengine/driver.cpp", "planning-path_planning_amd/csrc/planner.cpp",
+        "planning-path_planning_amd/csrc/local_layer.cpp")]
+    subprocess.run(["g++", *FLAGS, "-std=c++17", *inc, *srcs, *objs, "-o", exe, "-lm"],
+                   check=True)
+    return exe
+
+
+def _run(exe, mode, **env):
+    e = {k: v for k, v in os.environ.items() if k != "HOST_ENGINE_FAIL_D2H"}
+    e.update(env)
+    return subprocess.run([exe, mode], capture_output=True, text=True, env=e, timeout=300)
+
+
+def test_readback_matches_oracle(driver):
+    r = _run(driver, "ok")
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("nth", [1, 2, 9])
+def test_failed_chunk_download_throws(driver, nth):
+    """a d2h failure with no error text (dymu_last_error == "") in the
+    chunked readback must raise, on the first, second or a later chunk."""
+    r = _run(driver, "fail", HOST_ENGINE_FAIL_D2H=str(nth))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "threw" in r.stdout
+
+
+def test_engine_options_after_solve_keep_map(driver):
+    r = _run(driver, "options")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "options ok" in r.stdout
+
+
+def test_early_exit_with_ties(driver):
+    r = _run(driver, "ties")
+    assert r.returncode == 0, r.stdout + r.stderr
