@@ -1,18 +1,23 @@
 /*
- * dymu_dist.h -- C-ABI of the row-slab sharded solve driven natively (C++
- * loop, RCCL over xGMI on the engine's stream).
+ * dymu_dist.h -- C-ABI of the row-slab sharded solve driven natively (one C++
+ * round loop on the engine's stream, behind a transport).
  *
- * One process per GPU.  The global ny x nx grid is cut into row slabs
+ * One process per rank.  The global ny x nx grid is cut into row slabs
  * (dymu_slab_rows); rank r owns rows [row0, row0+nrows) and solves them with
  * the engine's domain primitives (dymu_dom_*, include/dymu_fim.h).  Every
  * `passes_per_exchange` passes (one round) the ranks swap their boundary rows
- * with rank-1 / rank+1 (grouped ncclSend/ncclRecv, nx x 8 B per neighbour),
- * min-merge them into their ghost rows and count the queued tiles in one launch
- * (dymu_dom_exchange), and on every 4th round all-reduce that count (4 bytes),
- * all on the engine's stream.  The host reads the all-reduced count of the
- * PREVIOUS check (pinned host copy + event), so the device always has work
- * queued.  A zero count after a round means the global fixed point was reached
- * (DESIGN.md s5).
+ * with rank-1 / rank+1 (nx x 8 B per neighbour), the next round's first pass
+ * min-merges them into the ghost rows, and on every 4th round the ranks reduce
+ * the round's queued-tile count (4 bytes); the host reads the reduced count of
+ * the PREVIOUS check through the engine's mailbox, so the device always has
+ * work queued.  A zero count after a round means the global fixed point was
+ * reached.  Transports (the same loop for all of them):
+ *   DYMU_DIST_RCCL  grouped ncclSend/ncclRecv over xGMI + ncclAllReduce, one GPU
+ *                   per rank (dymu_dist_create; the bench's multi-GPU path)
+ *   DYMU_DIST_IPC   rows pushed into the neighbours' hipIpc-mapped receive rows,
+ *                   counts reduced through a POSIX shared-memory board; ranks of
+ *                   one node, several per GPU allowed (dymu_dist_create_ipc)
+ *   virtual         all ranks in one process (dymu_vdist_solve)
  *
  * This replaces, for a grid too large or too slow for one GPU, the reference's
  * single-threaded propagation loop computeEntireTotalCostMap
@@ -36,6 +41,8 @@ extern "C" {
 #endif
 
 #define DYMU_DIST_ID_BYTES 128 /* sizeof(ncclUniqueId) */
+#define DYMU_DIST_RCCL 0
+#define DYMU_DIST_IPC 1
 
 typedef struct dymu_dist dymu_dist;
 
@@ -50,6 +57,17 @@ int dymu_dist_create(dymu_dist** out, dymu_ctx* ctx, int device,
                      const unsigned char id[DYMU_DIST_ID_BYTES], int rank, int world);
 int dymu_dist_destroy(dymu_dist* d);
 
+/* The IPC transport.  Rank 0 makes the id (the name of a fresh shared-memory
+ * board, /dev/shm) and the caller broadcasts its 128 bytes; creation is
+ * collective (returns once every rank has joined the board).  Every rank must
+ * run on the same node; the ranks may share a GPU.  Per round the host waits
+ * for its own push and both neighbours' (DYMU_DIST_TIMEOUT_S bounds each wait). */
+int dymu_dist_ipc_unique_id(unsigned char id[DYMU_DIST_ID_BYTES]);
+int dymu_dist_create_ipc(dymu_dist** out, dymu_ctx* ctx, int device,
+                         const unsigned char id[DYMU_DIST_ID_BYTES], int rank, int world);
+/* DYMU_DIST_RCCL or DYMU_DIST_IPC */
+int dymu_dist_transport(dymu_dist* d);
+
 /* Sharded solve of the global grid (nx x ny, goal (goal_i, goal_j) in global
  * coordinates); this rank's slab geometry comes from dymu_slab_rows.
  * Collective: every rank calls it with the same nx, ny, goal and
@@ -57,7 +75,7 @@ int dymu_dist_destroy(dymu_dist* d);
  * Blocks until converged; stats are this rank's (rounds = exchange rounds).
  * Errors: a collective pre-flight first checks every rank's arguments, so a
  * rank-local argument error returns DYMU_ERR_ARG on every rank.  Any later
- * error aborts the communicator (ncclCommAbort: peers blocked in an exchange
+ * error aborts the transport (ncclCommAbort for RCCL: peers blocked in an exchange
  * this rank will not post are released by their own wait timeout,
  * DYMU_DIST_TIMEOUT_S, default 300 s) and every further solve on this handle
  * returns DYMU_ERR_STATE. */
@@ -65,11 +83,11 @@ int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t 
                     uint32_t ny, uint32_t goal_i, uint32_t goal_j, uint32_t passes_per_exchange,
                     void* stream, dymu_stats* stats);
 
-/* The same loop with `world` virtual ranks in one process (tests, rehearsal):
- * ctxs[r] / F_slabs[r] / T_bufs[r] are rank r's context and slab buffers, all
- * on the current device; the exchange is device-to-device copies and the
- * all-reduce a host sum, all ordered on `stream` (required, not NULL).
- * stats: `world` entries (may be NULL). */
+/* The same loop with `world` (<= 16) virtual ranks in one process (tests,
+ * rehearsal): ctxs[r] / F_slabs[r] / T_bufs[r] are rank r's context and slab
+ * buffers, all on the current device; the exchange is device-to-device copies
+ * and the reduction a device sum posted through ctxs[0]'s mailbox, all ordered
+ * on `stream` (required, not NULL).  stats: `world` entries (may be NULL). */
 int dymu_vdist_solve(dymu_ctx* const* ctxs, int world, const double* const* F_slabs,
                      double* const* T_bufs, uint64_t ld, uint32_t nx, uint32_t ny,
                      uint32_t goal_i, uint32_t goal_j, uint32_t passes_per_exchange,
@@ -77,8 +95,8 @@ int dymu_vdist_solve(dymu_ctx* const* ctxs, int world, const double* const* F_sl
 
 const char* dymu_dist_last_error(dymu_dist* d);
 
-/* Ranks in the communicator (ncclCommCount): what RCCL actually sees, for the
- * bench line's `ranks_seen`. */
+/* Ranks in the communicator (ncclCommCount) or on the IPC board: what the
+ * transport actually sees, for the bench line's `ranks_seen`. */
 int dymu_dist_comm_count(dymu_dist* d, int* ranks);
 
 #ifdef __cplusplus

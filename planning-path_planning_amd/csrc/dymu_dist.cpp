@@ -1,20 +1,37 @@
 // dymu_dist.cpp -- row-slab sharded solve driven from C++ (include/dymu_dist.h).
 //
-// The loop the Python SlabSolver (dymu/sharded.py) runs over torch.distributed,
-// here natively, every step on the engine's stream.  Round m:
-//   K passes (dymu_dom_run)
-//   -> grouped ncclSend/ncclRecv: the first / last owned rows straight from T
-//      to rank-1 / rank+1, theirs into two receive rows
-//   -> one exchange launch: min-merge the received rows into the ghost rows and
-//      count the tiles queued for the next pass (dymu_dom_exchange)
-//   -> every kCheckEvery-th round: ncclAllReduce of that count -> 4-byte copy to
-//      pinned host memory + event.
-// The host reads the previous check's count after queueing the current one, so
-// it never drains the device queue; up to two check intervals of (empty) rounds
-// run after convergence.  With kernel-5 slabs (dymu_dom_round) the received rows
-// are instead merged by the next round's first pass -- no exchange launch -- and
-// the all-reduced count reaches the host through the engine's mailbox: the next
-// round's first pass stores it into host-coherent memory (no copy, no event).
+// ONE round loop (run_rounds) for every way the slabs can talk; a Transport
+// moves the boundary rows and reduces the termination count:
+//   RcclTransport     one rank per process, grouped ncclSend/ncclRecv of the
+//                     boundary rows over xGMI + ncclAllReduce of the count (the
+//                     bench's multi-GPU path, dymu_dist_solve)
+//   IpcTransport      one rank per process, the rows pushed into the neighbours'
+//                     hipIpc-mapped receive rows, the count reduced through a
+//                     host shared-memory board (dymu_dist_create_ipc; runs with
+//                     several ranks on ONE GPU, where RCCL refuses duplicates)
+//   VirtualTransport  every rank in one process on one stream, device-to-device
+//                     row copies and a device sum (dymu_vdist_solve: rehearsal)
+// so the tests of the IPC and virtual transports run the loop, the pre-flight,
+// the fused rounds and the mailbox posts that the RCCL bench runs.  Round m:
+//   K passes (dymu_dom_round: the first pass min-merges the rows received after
+//   round m-1 into the ghost rows; the second writes the round's count = tiles
+//   queued for the first + for the second pass)
+//   -> exchange: the first / last owned rows to rank-1 / rank+1
+//   -> every kCheckEvery-th round: reduce the count over the ranks; the next
+//      round's first pass posts it into the engine's host-coherent mailbox
+//      (dymu_dom_post); the host reads the PREVIOUS check's post after queueing
+//      this one, so the device queue never drains.
+// A zero global count after a round is the fixed point: no rank had a tile
+// queued after round m-1, and the rows the ranks held after round m-1 (merged
+// in round m) improved no ghost row -- so every ghost row equals its
+// neighbour's final row and every slab is converged against it.  The exchange
+// must therefore deliver, before round m+1's merge, rows at least as new as the
+// sender's state after round m: RCCL orders the receive after the send on both
+// streams, the virtual copies are on the one stream, and the IPC push is
+// host-synchronised per round (exchange() returns once this rank's push of
+// round m completed and both neighbours have reported theirs).
+// Kernel 3/4 slabs (no fused round) keep the v1 round: dymu_dom_run, the
+// transfer, then one dymu_dom_exchange launch that merges and counts.
 //
 // Why one stream and no overlap: the pass kernel is one 1024-thread workgroup
 // per CU at full register use, back to back, so a kernel on a second stream
@@ -27,56 +44,39 @@
 // is propagateGlobalNode (:500-546).  SURVEY.md s8(e).
 #include "dymu_dist.h"
 
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <random>
 #include <string>
 #include <thread>
 #include <vector>
 
-// Per-rank exchange buffers: r = the rows received from rank-1 (side 0) and
-// rank+1 (side 1); d_cnt = [queued tiles of this round, its all-reduced value]
-// for two round parities (the host reads round m-1's while round m is queued).
-struct Pipe {
-  double* rbuf = nullptr;    // [2 side][cap]
-  int32_t* d_cnt = nullptr;  // [2 parity][2], then the pre-flight flag
-  uint64_t cap = 0;
-  double* r(int side) const { return rbuf + (uint64_t)side * cap; }
-  int32_t* tot(int par) const { return d_cnt + 2 * par; }
-  int32_t* sum(int par) const { return d_cnt + 2 * par + 1; }
-  int32_t* flag() const { return d_cnt + 4; }
-};
-
-struct dymu_dist {
-  dymu_ctx* ctx = nullptr;
-  int device = 0;
-  int rank = 0, world = 1;
-  ncclComm_t comm = nullptr;
-  bool aborted = false;  // the communicator was aborted after an error (no further solves)
-  Pipe pipe;
-  int32_t* h_sum = nullptr;  // pinned [2 parity + the pre-flight flag]
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  std::string last_error;
-};
+#include "fim_kernels.h"
 
 namespace {
 
-// passes per round: a round costs one RCCL P2P group + one exchange launch + one
-// 4-byte all-reduce on the pass stream (~8 us at N=1 without the P2P), and ghost
-// rows are at most K passes stale.  16384^2 rehearsal (tools/vdist_rehearsal.py,
-// max per-rank pass time): K = 4 -> 37.4 / 27.4 / 21.8 ms at 2 / 4 / 8 ranks in
-// 338 / 327 / 302 rounds; K = 8 -> 44.6 / 32.8 / 27.2 ms in 156 / 163 / 156.
+// passes per round: a round costs one exchange + (every 4th round) one 4-byte
+// reduction on the pass stream, and ghost rows are at most K passes stale.
+// 16384^2 rehearsal (tools/vdist_rehearsal.py, max per-rank pass time, v26):
+// K = 2 / 3 / 4 / 6 / 8 -> 26.6 / 26.5 / 26.4 / 27.4 / 30.4 ms at 2 ranks
+// (profiles/r02/vdist_K_v26.txt).
 constexpr uint32_t kDefaultK = 4;
-// rounds per termination check: the 4-byte all-reduce (and its copy to the host)
-// sits on the pass stream, so it runs on every kCheckEvery-th round only.  A zero
-// global count after ANY round is the fixed point (no rank has work and no ghost
-// improved), so checking a subset of rounds is exact; the solve ends at most two
+// rounds per termination check: a zero global count after ANY round is the fixed
+// point, so checking a subset of rounds is exact; the solve ends at most two
 // check intervals of empty rounds later.
 constexpr uint64_t kCheckEvery = 4;
+// ranks of one shared-memory board / one virtual world
+constexpr int kMaxWorld = 64;
 
 int fail(std::string* err, const char* what, const char* detail, int code) {
   if (err) {
@@ -106,6 +106,48 @@ int fail(std::string* err, const char* what, const char* detail, int code) {
     int _rc = (expr);               \
     if (_rc != DYMU_OK) return _rc; \
   } while (0)
+
+// Host waits on a peer (an event queued behind RCCL work, a board entry another
+// process writes) are bounded: a peer that died or left the sequence would
+// otherwise block this rank forever.  DYMU_DIST_TIMEOUT_S (default 300 s).
+double dist_timeout_s() {
+  static const double limit_s = [] {
+    const char* kv = std::getenv("DYMU_DIST_TIMEOUT_S");
+    const double v = kv ? std::atof(kv) : 0.0;
+    return v > 0.0 ? v : 300.0;
+  }();
+  return limit_s;
+}
+
+// spin on cond() with a pause, then short sleeps; false after the timeout
+template <class Cond>
+bool spin_until(Cond&& cond) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 0;; ++spin) {
+    if (cond()) return true;
+    if (spin > 256) std::this_thread::sleep_for(std::chrono::microseconds(20));
+#if defined(__x86_64__)
+    else __builtin_ia32_pause();
+#endif
+    if ((spin & 255) == 255 &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >
+            dist_timeout_s())
+      return false;
+  }
+}
+
+int wait_event(hipEvent_t ev, std::string* err) {
+  hipError_t e = hipErrorNotReady;
+  const bool ok = spin_until([&] {
+    e = hipEventQuery(ev);
+    return e != hipErrorNotReady;
+  });
+  if (!ok)
+    return fail(err, "dymu_dist_solve", "timed out waiting for the exchange (a peer rank failed?)",
+                DYMU_ERR_RCCL);
+  if (e != hipSuccess) return fail(err, "hipEventQuery", hipGetErrorString(e), DYMU_ERR_HIP);
+  return DYMU_OK;
+}
 
 // geometry of one rank's slab and its domain descriptor
 struct Slab {
@@ -141,49 +183,486 @@ uint64_t max_rounds(uint32_t nx, uint32_t ny, uint32_t K) {
   return (4 * t8 + 1024) / K + 4;
 }
 
-int pipe_alloc(Pipe* p, uint64_t nx) {
-  if (p->cap >= nx) return DYMU_OK;
-  if (p->rbuf) (void)hipFree(p->rbuf);
-  if (p->d_cnt) (void)hipFree(p->d_cnt);
-  *p = Pipe{};
-  if (hipMalloc(&p->rbuf, sizeof(double) * 2 * nx) != hipSuccess ||
-      hipMalloc(&p->d_cnt, sizeof(int32_t) * 5) != hipSuccess)
-    return DYMU_ERR_NOMEM;
-  p->cap = nx;
+// A rank this process drives: its context, slab and receive rows (owned by the
+// transport; side 0 = rank-1's last row, side 1 = rank+1's first row).
+struct Local {
+  dymu_ctx* ctx = nullptr;
+  int rank = 0;
+  Slab s;
+  double* recv = nullptr;
+  uint64_t cap = 0;
+  double* r(int side) const { return recv + (uint64_t)side * cap; }
+};
+
+// Per-round counts live in device memory the transport owns: tot(l, par) is
+// what local rank l's round writes at a check of parity par, post_src(par) the
+// device word the check's mailbox post carries (the reduced count, or the local
+// one when the transport reduces on the host, combine()).
+class Transport {
+ public:
+  virtual ~Transport() = default;
+  // receive rows and count words for an nx-wide grid (local; sets L[l].recv)
+  virtual int alloc(std::vector<Local>& L, uint32_t nx, std::string* err) = 0;
+  // collective: every rank learns whether every rank can solve
+  virtual int preflight(bool ok, hipStream_t st, std::string* err) = 0;
+  // collective, after a successful pre-flight: peers' buffers mapped
+  virtual int connect(std::string* err) {
+    (void)err;
+    return DYMU_OK;
+  }
+  virtual int32_t* tot(int l, int par) = 0;
+  virtual const int32_t* post_src(int par) = 0;
+  virtual int exchange(std::vector<Local>& L, uint32_t nx, hipStream_t st, std::string* err) = 0;
+  virtual int reduce(int par, hipStream_t st, std::string* err) = 0;
+  virtual int combine(int32_t posted, int64_t* global, std::string* err) {
+    (void)err;
+    *global = posted;
+    return DYMU_OK;
+  }
+  virtual int ranks_seen() = 0;
+  // after an error inside the collective sequence (peers may be blocked)
+  virtual void abort() {}
+};
+
+// pinned host words + events of the fallback checks (a context without a mailbox)
+struct LoopRes {
+  int32_t* h = nullptr;  // [2 parity + 1 pre-flight]
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  int init(std::string* err) {
+    if (h) return DYMU_OK;
+    DHIP(err, hipHostMalloc(&h, sizeof(int32_t) * 3, hipHostMallocDefault));
+    for (auto& e : ev) DHIP(err, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return DYMU_OK;
+  }
+  ~LoopRes() {
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (h) (void)hipHostFree(h);
+  }
+};
+
+// ---- the round loop (the domains are live on entry) ----
+// An error return leaves the collective sequence in an unknown state; the caller
+// aborts the transport.
+int run_rounds(std::vector<Local>& L, Transport& X, LoopRes& R, uint32_t nx, uint32_t ny,
+               uint32_t K, hipStream_t st, std::string* err, uint64_t* rounds) {
+  const uint64_t cap = max_rounds(nx, ny, K) + 2 * kCheckEvery;
+  // fused: the rows received after round m are merged by round m+1's first pass
+  // (dymu_dom_round) instead of a dymu_dom_exchange launch after the transfer
+  bool fused = true;
+  for (auto& l : L) fused = fused && dymu_dom_round_supported(l.ctx, K) == 1;
+  dymu_ctx* mctx = L[0].ctx;  // the first local rank's mailbox carries the checks
+  bool mail = true;
+  uint32_t prev_seq = 0;
+  uint64_t m = 0, checks = 0;
+  bool done = false, have_rows = false;
+  for (; !done; ++m) {
+    if (m >= cap)
+      return fail(err, "dymu_dist_solve", "exchange-round cap reached", DYMU_ERR_NOT_CONVERGED);
+    const bool check = (m % kCheckEvery) == kCheckEvery - 1;
+    const int par = (int)(checks & 1);
+    for (size_t q = 0; q < L.size(); ++q) {
+      const Local& l = L[q];
+      const int rc =
+          fused ? dymu_dom_round(l.ctx, K, have_rows && l.s.lo ? l.r(0) : nullptr,
+                                 have_rows && l.s.hi ? l.r(1) : nullptr, X.tot((int)q, par), st)
+                : dymu_dom_run(l.ctx, K, st);
+      if (rc) return fail(err, fused ? "dymu_dom_round" : "dymu_dom_run", dymu_last_error(l.ctx), rc);
+    }
+    DCALL(X.exchange(L, nx, st, err));
+    have_rows = true;
+    if (!fused) {
+      for (size_t q = 0; q < L.size(); ++q) {
+        const Local& l = L[q];
+        const int rc = dymu_dom_exchange(l.ctx, l.s.lo ? l.r(0) : nullptr,
+                                         l.s.hi ? l.r(1) : nullptr, X.tot((int)q, par), st);
+        if (rc) return fail(err, "dymu_dom_exchange", dymu_last_error(l.ctx), rc);
+      }
+    }
+    if (!check) continue;
+    DCALL(X.reduce(par, st, err));
+    if (mail) {  // the next round's first pass posts the count; read the previous check's
+      uint32_t seq = 0;
+      const int rc = dymu_dom_post(mctx, X.post_src(par), &seq);
+      if (rc == DYMU_ERR_STATE && checks == 0) {
+        mail = false;
+      } else if (rc) {
+        return fail(err, "dymu_dom_post", dymu_last_error(mctx), rc);
+      } else {
+        if (checks >= 1) {
+          int32_t v = 0;
+          if (dymu_dom_wait_post(mctx, prev_seq, dist_timeout_s(), &v, st) != DYMU_OK)
+            return fail(err, "dymu_dom_wait_post", dymu_last_error(mctx), DYMU_ERR_RCCL);
+          int64_t g = 0;
+          DCALL(X.combine(v, &g, err));
+          done = g == 0;
+        }
+        prev_seq = seq;
+      }
+    }
+    if (!mail) {
+      DCALL(R.init(err));
+      DHIP(err, hipMemcpyAsync(R.h + par, X.post_src(par), sizeof(int32_t), hipMemcpyDeviceToHost,
+                               st));
+      DHIP(err, hipEventRecord(R.ev[par], st));
+      if (checks >= 1) {  // the previous check's count; this one stays queued meanwhile
+        DCALL(wait_event(R.ev[par ^ 1], err));
+        int64_t g = 0;
+        DCALL(X.combine(R.h[par ^ 1], &g, err));
+        done = g == 0;
+      }
+    }
+    ++checks;
+  }
+  *rounds = m;
   return DYMU_OK;
 }
 
-void pipe_free(Pipe* p) {
-  if (p->rbuf) (void)hipFree(p->rbuf);
-  if (p->d_cnt) (void)hipFree(p->d_cnt);
-  *p = Pipe{};
-}
+// ---------------------------------------------------------------------------
+// RCCL: grouped ncclSend/ncclRecv + ncclAllReduce, all on the engine's stream
+// ---------------------------------------------------------------------------
+class RcclTransport final : public Transport {
+ public:
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1;
+  double* rbuf = nullptr;    // [2 side][cap]
+  int32_t* d_cnt = nullptr;  // [2 parity][tot, sum], then the pre-flight flag
+  uint64_t cap = 0;
+  LoopRes pre;
 
-// Host wait on an event queued behind RCCL work, bounded: a peer that died or
-// left the collective sequence would otherwise block this rank forever.
-// DYMU_DIST_TIMEOUT_S (default 300 s) bounds one wait.
-double dist_timeout_s() {
-  static const double limit_s = [] {
-    const char* kv = std::getenv("DYMU_DIST_TIMEOUT_S");
-    const double v = kv ? std::atof(kv) : 0.0;
-    return v > 0.0 ? v : 300.0;
-  }();
-  return limit_s;
-}
-
-int wait_event(hipEvent_t ev, std::string* err) {
-  const double limit_s = dist_timeout_s();
-  const auto t0 = std::chrono::steady_clock::now();
-  for (unsigned spin = 0;; ++spin) {
-    const hipError_t e = hipEventQuery(ev);
-    if (e == hipSuccess) return DYMU_OK;
-    if (e != hipErrorNotReady) return fail(err, "hipEventQuery", hipGetErrorString(e), DYMU_ERR_HIP);
-    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
-    if ((spin & 1023) == 1023 &&
-        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s)
-      return fail(err, "dymu_dist_solve", "timed out waiting for the exchange (a peer rank failed?)",
-                  DYMU_ERR_RCCL);
+  ~RcclTransport() override {
+    if (comm) (void)ncclCommDestroy(comm);
+    release();
   }
+  void release() {
+    if (rbuf) (void)hipFree(rbuf);
+    if (d_cnt) (void)hipFree(d_cnt);
+    rbuf = nullptr;
+    d_cnt = nullptr;
+    cap = 0;
+  }
+  int alloc(std::vector<Local>& L, uint32_t nx, std::string* err) override {
+    if (cap < nx) {
+      release();
+      DHIP(err, hipMalloc(&rbuf, sizeof(double) * 2 * (uint64_t)nx));
+      DHIP(err, hipMalloc(&d_cnt, sizeof(int32_t) * 5));
+      cap = nx;
+    }
+    L[0].recv = rbuf;
+    L[0].cap = cap;
+    return DYMU_OK;
+  }
+  int preflight(bool ok, hipStream_t st, std::string* err) override {
+    DCALL(pre.init(err));
+    int32_t* flag = d_cnt + 4;
+    pre.h[2] = ok ? 1 : 0;
+    DHIP(err, hipMemcpyAsync(flag, pre.h + 2, sizeof(int32_t), hipMemcpyHostToDevice, st));
+    DNCCL(err, ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, comm, st));
+    DHIP(err, hipMemcpyAsync(pre.h + 2, flag, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    DHIP(err, hipEventRecord(pre.ev[0], st));
+    DCALL(wait_event(pre.ev[0], err));
+    if (pre.h[2] != 1)
+      return fail(err, "dymu_dist_solve", ok ? "another rank rejected its slab" : "invalid slab",
+                  DYMU_ERR_ARG);
+    return DYMU_OK;
+  }
+  int32_t* tot(int, int par) override { return d_cnt + 2 * par; }
+  const int32_t* post_src(int par) override { return d_cnt + 2 * par + 1; }
+  int exchange(std::vector<Local>& L, uint32_t nx, hipStream_t st, std::string* err) override {
+    const Local& l = L[0];
+    if (!l.s.lo && !l.s.hi) return DYMU_OK;
+    DNCCL(err, ncclGroupStart());
+    if (l.s.lo) {
+      DNCCL(err, ncclSend(l.s.row(0), nx, ncclDouble, rank - 1, comm, st));
+      DNCCL(err, ncclRecv(l.r(0), nx, ncclDouble, rank - 1, comm, st));
+    }
+    if (l.s.hi) {
+      DNCCL(err, ncclSend(l.s.row(1), nx, ncclDouble, rank + 1, comm, st));
+      DNCCL(err, ncclRecv(l.r(1), nx, ncclDouble, rank + 1, comm, st));
+    }
+    DNCCL(err, ncclGroupEnd());
+    return DYMU_OK;
+  }
+  int reduce(int par, hipStream_t st, std::string* err) override {
+    DNCCL(err, ncclAllReduce(d_cnt + 2 * par, d_cnt + 2 * par + 1, 1, ncclInt32, ncclSum, comm, st));
+    return DYMU_OK;
+  }
+  int ranks_seen() override {
+    int n = 0;
+    return comm && ncclCommCount(comm, &n) == ncclSuccess ? n : 0;
+  }
+  void abort() override {
+    if (comm) (void)ncclCommAbort(comm);
+    comm = nullptr;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// IPC: rows pushed into the neighbours' hipIpc-mapped receive rows, counts
+// reduced through a board in POSIX shared memory (/dev/shm); one node, any
+// number of ranks per GPU.  Per round the host waits for its own push and for
+// both neighbours' (the exactness condition in the header comment); the
+// reduction is a host sum over the board.
+// ---------------------------------------------------------------------------
+struct BoardSlot {
+  std::atomic<uint64_t> gen;       // generation of the published receive buffer
+  std::atomic<uint64_t> cap;       // its elements per side
+  std::atomic<uint64_t> pre;       // (solve << 1) | ok
+  std::atomic<uint64_t> pushed;    // rounds whose push completed (running count)
+  std::atomic<uint64_t> check[4];  // ((check + 1) << 32) | count, slot check % 4
+  std::atomic<uint64_t> joined;    // 1 once the rank opened the board
+  unsigned char handle[HIP_IPC_HANDLE_SIZE];
+  unsigned char pad[256 - 9 * 8 - HIP_IPC_HANDLE_SIZE];
+};
+static_assert(sizeof(BoardSlot) == 256, "board slot");
+static_assert(std::atomic<uint64_t>::is_always_lock_free, "board atomics");
+
+class IpcTransport final : public Transport {
+ public:
+  int rank = 0, world = 1;
+  std::string name;
+  bool owner = false;
+  BoardSlot* board = nullptr;
+  size_t board_bytes = 0;
+  double* recv = nullptr;  // [2 side][cap], exported
+  uint64_t cap = 0;
+  uint64_t gen = 0;        // generation of recv
+  int32_t* d_cnt = nullptr;  // [2 parity] local counts
+  double* peer[2] = {nullptr, nullptr};  // rank-1's / rank+1's receive rows (mapped)
+  uint64_t peer_gen[2] = {0, 0}, peer_cap[2] = {0, 0};
+  uint64_t solves = 0, rounds = 0, checks = 0;
+  hipEvent_t ev = nullptr;
+
+  ~IpcTransport() override {
+    for (auto& p : peer)
+      if (p) (void)hipIpcCloseMemHandle(p);
+    if (recv) (void)hipFree(recv);
+    if (d_cnt) (void)hipFree(d_cnt);
+    if (ev) (void)hipEventDestroy(ev);
+    if (board) munmap(board, board_bytes);
+    if (owner && !name.empty()) shm_unlink(name.c_str());
+  }
+  int open(const char* shm, int r, int w, std::string* err) {
+    rank = r;
+    world = w;
+    name = shm;
+    owner = r == 0;
+    board_bytes = sizeof(BoardSlot) * kMaxWorld;
+    const int fd = shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
+    if (fd < 0) return fail(err, "shm_open", std::strerror(errno), DYMU_ERR_STATE);
+    if (ftruncate(fd, (off_t)board_bytes) != 0) {
+      close(fd);
+      return fail(err, "ftruncate", std::strerror(errno), DYMU_ERR_STATE);
+    }
+    void* p = mmap(nullptr, board_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) return fail(err, "mmap", std::strerror(errno), DYMU_ERR_STATE);
+    board = static_cast<BoardSlot*>(p);
+    DHIP(err, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    DHIP(err, hipMalloc(&d_cnt, sizeof(int32_t) * 2));
+    // collective, like ncclCommInitRank: every rank has joined on return
+    board[rank].joined.store(1, std::memory_order_release);
+    for (int q = 0; q < world; ++q)
+      if (!spin_until([&] { return board[q].joined.load(std::memory_order_acquire) != 0; }))
+        return fail(err, "dymu_dist_create_ipc", "timed out waiting for the other ranks",
+                    DYMU_ERR_RCCL);
+    return DYMU_OK;
+  }
+  int alloc(std::vector<Local>& L, uint32_t nx, std::string* err) override {
+    if (cap < nx) {
+      if (recv) DHIP(err, hipFree(recv));
+      recv = nullptr;
+      cap = 0;
+      DHIP(err, hipMalloc(&recv, sizeof(double) * 2 * (uint64_t)nx));
+      cap = nx;
+      ++gen;
+    }
+    L[0].recv = recv;
+    L[0].cap = cap;
+    return DYMU_OK;
+  }
+  int preflight(bool ok, hipStream_t, std::string* err) override {
+    const uint64_t s = ++solves;
+    board[rank].pre.store((s << 1) | (ok ? 1u : 0u), std::memory_order_release);
+    bool all = true;
+    for (int q = 0; q < world; ++q) {
+      if (!spin_until([&] { return (board[q].pre.load(std::memory_order_acquire) >> 1) >= s; }))
+        return fail(err, "dymu_dist_solve", "timed out in the pre-flight (a peer rank failed?)",
+                    DYMU_ERR_RCCL);
+      all = all && (board[q].pre.load(std::memory_order_acquire) & 1u);
+    }
+    if (!all)
+      return fail(err, "dymu_dist_solve", ok ? "another rank rejected its slab" : "invalid slab",
+                  DYMU_ERR_ARG);
+    return DYMU_OK;
+  }
+  int connect(std::string* err) override {
+    if (board[rank].gen.load(std::memory_order_acquire) != gen) {  // publish a new buffer
+      hipIpcMemHandle_t h;
+      DHIP(err, hipIpcGetMemHandle(&h, recv));
+      std::memcpy(board[rank].handle, &h, sizeof h);
+      board[rank].cap.store(cap, std::memory_order_relaxed);
+      board[rank].gen.store(gen, std::memory_order_release);
+    }
+    for (int side = 0; side < 2; ++side) {
+      const int q = side == 0 ? rank - 1 : rank + 1;
+      if (q < 0 || q >= world) continue;
+      // every rank allocates at the same solves (same nx sequence): same generation
+      if (!spin_until([&] { return board[q].gen.load(std::memory_order_acquire) >= gen; }))
+        return fail(err, "dymu_dist_solve", "timed out waiting for a peer's receive rows",
+                    DYMU_ERR_RCCL);
+      const uint64_t g = board[q].gen.load(std::memory_order_acquire);
+      if (g == peer_gen[side] && peer[side]) continue;
+      if (peer[side]) DHIP(err, hipIpcCloseMemHandle(peer[side]));
+      peer[side] = nullptr;
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, board[q].handle, sizeof h);
+      void* p = nullptr;
+      DHIP(err, hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+      peer[side] = static_cast<double*>(p);
+      peer_gen[side] = g;
+      peer_cap[side] = board[q].cap.load(std::memory_order_relaxed);
+    }
+    return DYMU_OK;
+  }
+  int32_t* tot(int, int par) override { return d_cnt + par; }
+  const int32_t* post_src(int par) override { return d_cnt + par; }
+  int exchange(std::vector<Local>& L, uint32_t nx, hipStream_t st, std::string* err) override {
+    const Local& l = L[0];
+    // push: my first row into rank-1's "from rank+1" row, my last into rank+1's
+    // "from rank-1" row (ordered after this round's passes on my stream)
+    if (l.s.lo)
+      DHIP(err, hipMemcpyAsync(peer[0] + peer_cap[0], l.s.row(0), sizeof(double) * nx,
+                               hipMemcpyDeviceToDevice, st));
+    if (l.s.hi)
+      DHIP(err, hipMemcpyAsync(peer[1], l.s.row(1), sizeof(double) * nx, hipMemcpyDeviceToDevice,
+                               st));
+    const uint64_t m = ++rounds;
+    if (!l.s.lo && !l.s.hi) return DYMU_OK;
+    DHIP(err, hipEventRecord(ev, st));
+    DCALL(wait_event(ev, err));
+    board[rank].pushed.store(m, std::memory_order_release);
+    for (int side = 0; side < 2; ++side) {
+      const int q = side == 0 ? rank - 1 : rank + 1;
+      if ((side == 0 && !l.s.lo) || (side == 1 && !l.s.hi)) continue;
+      if (!spin_until([&] { return board[q].pushed.load(std::memory_order_acquire) >= m; }))
+        return fail(err, "dymu_dist_solve", "timed out waiting for a neighbour's rows",
+                    DYMU_ERR_RCCL);
+    }
+    return DYMU_OK;
+  }
+  int reduce(int, hipStream_t, std::string*) override { return DYMU_OK; }
+  int combine(int32_t posted, int64_t* global, std::string* err) override {
+    const uint64_t c = checks++;
+    const uint64_t tag = (c + 1) << 32;
+    board[rank].check[c % 4].store(tag | (uint32_t)posted, std::memory_order_release);
+    int64_t g = 0;
+    for (int q = 0; q < world; ++q) {
+      uint64_t v = 0;
+      if (!spin_until([&] {
+            v = board[q].check[c % 4].load(std::memory_order_acquire);
+            return (v >> 32) >= c + 1;
+          }))
+        return fail(err, "dymu_dist_solve", "timed out in the count reduction", DYMU_ERR_RCCL);
+      g += (int64_t)(uint32_t)v;
+    }
+    *global = g;
+    return DYMU_OK;
+  }
+  int ranks_seen() override {  // ranks that joined the board
+    int n = 0;
+    for (int q = 0; q < kMaxWorld; ++q) n += board[q].joined.load(std::memory_order_acquire) ? 1 : 0;
+    return n;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Virtual ranks: every rank in this process, one stream; D2D copies for the
+// rows, the count summed on the device (k_sum_counts over 16 words per parity)
+// ---------------------------------------------------------------------------
+class VirtualTransport final : public Transport {
+ public:
+  std::vector<double*> rows;
+  uint32_t* cnt = nullptr;  // [2 parity][16]: tot of local rank l at [par][l]
+  int32_t* sum = nullptr;   // [2 parity]
+
+  ~VirtualTransport() override {
+    for (double* p : rows)
+      if (p) (void)hipFree(p);
+    if (cnt) (void)hipFree(cnt);
+    if (sum) (void)hipFree(sum);
+  }
+  int alloc(std::vector<Local>& L, uint32_t nx, std::string* err) override {
+    if ((int)L.size() > dymu::kShards)
+      return fail(err, "dymu_vdist_solve", "at most 16 virtual ranks", DYMU_ERR_ARG);
+    rows.assign(L.size(), nullptr);
+    for (size_t q = 0; q < L.size(); ++q) {
+      DHIP(err, hipMalloc(&rows[q], sizeof(double) * 2 * (uint64_t)nx));
+      L[q].recv = rows[q];
+      L[q].cap = nx;
+    }
+    DHIP(err, hipMalloc(&cnt, sizeof(uint32_t) * 2 * dymu::kShards));
+    DHIP(err, hipMemset(cnt, 0, sizeof(uint32_t) * 2 * dymu::kShards));
+    DHIP(err, hipMalloc(&sum, sizeof(int32_t) * 2));
+    return DYMU_OK;
+  }
+  int preflight(bool ok, hipStream_t, std::string* err) override {
+    return ok ? DYMU_OK : fail(err, "dymu_vdist_solve", "invalid slab", DYMU_ERR_ARG);
+  }
+  int32_t* tot(int l, int par) override {
+    return reinterpret_cast<int32_t*>(cnt + par * dymu::kShards + l);
+  }
+  const int32_t* post_src(int par) override { return sum + par; }
+  int exchange(std::vector<Local>& L, uint32_t nx, hipStream_t st, std::string* err) override {
+    for (size_t q = 0; q < L.size(); ++q) {  // rank q-1's last row / rank q+1's first row
+      if (L[q].s.lo)
+        DHIP(err, hipMemcpyAsync(L[q].r(0), L[q - 1].s.row(1), sizeof(double) * nx,
+                                 hipMemcpyDeviceToDevice, st));
+      if (L[q].s.hi)
+        DHIP(err, hipMemcpyAsync(L[q].r(1), L[q + 1].s.row(0), sizeof(double) * nx,
+                                 hipMemcpyDeviceToDevice, st));
+    }
+    return DYMU_OK;
+  }
+  int reduce(int par, hipStream_t st, std::string* err) override {
+    DHIP(err, dymu::launch_sum_counts(cnt + par * dymu::kShards, sum + par, st));
+    return DYMU_OK;
+  }
+  int ranks_seen() override { return (int)rows.size(); }
+};
+
+}  // namespace
+
+struct dymu_dist {
+  dymu_ctx* ctx = nullptr;
+  int device = 0;
+  int rank = 0, world = 1;
+  int kind = DYMU_DIST_RCCL;
+  std::unique_ptr<Transport> xp;
+  LoopRes res;
+  bool aborted = false;  // the transport was aborted after an error (no further solves)
+  std::string last_error;
+};
+
+namespace {
+
+// After an error inside the collective sequence: abort the transport (its peers
+// may be blocked in an exchange this rank will never post; they are released by
+// their own wait timeout), and refuse further solves on this handle.
+int abort_dist(dymu_dist* d, int rc) {
+  if (d->xp) d->xp->abort();
+  d->aborted = true;
+  return rc;
+}
+
+dymu_dist* new_dist(dymu_ctx* ctx, int device, int rank, int world, int kind) {
+  auto* d = new dymu_dist;
+  d->ctx = ctx;
+  d->device = device;
+  d->rank = rank;
+  d->world = world;
+  d->kind = kind;
+  return d;
 }
 
 }  // namespace
@@ -203,25 +682,57 @@ int dymu_dist_create(dymu_dist** out, dymu_ctx* ctx, int device,
                      const unsigned char id[DYMU_DIST_ID_BYTES], int rank, int world) {
   if (!out || !ctx || !id || world < 1 || rank < 0 || rank >= world) return DYMU_ERR_ARG;
   *out = nullptr;
-  auto* d = new dymu_dist;
-  d->ctx = ctx;
-  d->device = device;
-  d->rank = rank;
-  d->world = world;
+  dymu_dist* d = new_dist(ctx, device, rank, world, DYMU_DIST_RCCL);
   auto bail = [&](int rc) {
     dymu_dist_destroy(d);
     return rc;
   };
   if (hipSetDevice(device) != hipSuccess) return bail(DYMU_ERR_HIP);
-  if (hipHostMalloc(&d->h_sum, sizeof(int32_t) * 3, hipHostMallocDefault) != hipSuccess)
-    return bail(DYMU_ERR_NOMEM);
-  for (auto& e : d->ev)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return bail(DYMU_ERR_HIP);
+  auto x = std::make_unique<RcclTransport>();
+  x->rank = rank;
+  x->world = world;
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof u);
-  if (ncclCommInitRank(&d->comm, world, u, rank) != ncclSuccess) {
-    d->comm = nullptr;
+  if (ncclCommInitRank(&x->comm, world, u, rank) != ncclSuccess) {
+    x->comm = nullptr;
     return bail(DYMU_ERR_RCCL);
+  }
+  d->xp = std::move(x);
+  *out = d;
+  return DYMU_OK;
+}
+
+int dymu_dist_ipc_unique_id(unsigned char id[DYMU_DIST_ID_BYTES]) {
+  if (!id) return DYMU_ERR_ARG;
+  std::random_device rd;
+  char name[64];
+  std::snprintf(name, sizeof name, "/dymu_ipc_%d_%08x%08x", (int)getpid(), (unsigned)rd(),
+                (unsigned)rd());
+  std::memset(id, 0, DYMU_DIST_ID_BYTES);
+  std::memcpy(id, name, std::strlen(name));
+  return DYMU_OK;
+}
+
+int dymu_dist_create_ipc(dymu_dist** out, dymu_ctx* ctx, int device,
+                         const unsigned char id[DYMU_DIST_ID_BYTES], int rank, int world) {
+  if (!out || !ctx || !id || world < 1 || world > kMaxWorld || rank < 0 || rank >= world)
+    return DYMU_ERR_ARG;
+  *out = nullptr;
+  char name[DYMU_DIST_ID_BYTES + 1];
+  std::memcpy(name, id, DYMU_DIST_ID_BYTES);
+  name[DYMU_DIST_ID_BYTES] = 0;
+  if (name[0] != '/' || std::strchr(name + 1, '/')) return DYMU_ERR_ARG;
+  dymu_dist* d = new_dist(ctx, device, rank, world, DYMU_DIST_IPC);
+  if (hipSetDevice(device) != hipSuccess) {
+    dymu_dist_destroy(d);
+    return DYMU_ERR_HIP;
+  }
+  auto x = std::make_unique<IpcTransport>();
+  const int rc = x->open(name, rank, world, &d->last_error);
+  d->xp = std::move(x);
+  if (rc) {
+    dymu_dist_destroy(d);
+    return rc;
   }
   *out = d;
   return DYMU_OK;
@@ -230,167 +741,56 @@ int dymu_dist_create(dymu_dist** out, dymu_ctx* ctx, int device,
 int dymu_dist_destroy(dymu_dist* d) {
   if (!d) return DYMU_OK;
   (void)hipSetDevice(d->device);
-  if (d->comm) (void)ncclCommDestroy(d->comm);
-  for (auto& e : d->ev)
-    if (e) (void)hipEventDestroy(e);
-  pipe_free(&d->pipe);
-  if (d->h_sum) (void)hipHostFree(d->h_sum);
+  d->xp.reset();
   delete d;
   return DYMU_OK;
 }
 
 const char* dymu_dist_last_error(dymu_dist* d) { return d ? d->last_error.c_str() : ""; }
 
+int dymu_dist_transport(dymu_dist* d) { return d ? d->kind : DYMU_ERR_ARG; }
+
 int dymu_dist_comm_count(dymu_dist* d, int* ranks) {
   if (!d || !ranks) return DYMU_ERR_ARG;
-  if (!d->comm) return DYMU_ERR_STATE;
-  int n = 0;
-  if (ncclCommCount(d->comm, &n) != ncclSuccess) return DYMU_ERR_RCCL;
+  if (!d->xp || d->aborted) return DYMU_ERR_STATE;
+  const int n = d->xp->ranks_seen();
+  if (n <= 0) return DYMU_ERR_RCCL;
   *ranks = n;
   return DYMU_OK;
 }
-
-}  // extern "C"
-
-namespace {
-
-// The round loop of dymu_dist_solve (the domain is live on entry).  Any error
-// return leaves the communicator in an unknown collective state; the caller
-// aborts it.
-int dist_rounds(dymu_dist* d, const Slab& s, uint32_t nx, uint32_t ny, uint32_t K, void* stream,
-                uint64_t* rounds) {
-  std::string* err = &d->last_error;
-  const Pipe& p = d->pipe;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  const uint64_t cap = max_rounds(nx, ny, K) + 2 * kCheckEvery;
-  // fused: the rows received after round m are merged by round m+1's first pass
-  // (dymu_dom_round) instead of a k_exchange launch after the transfer
-  const bool fused = dymu_dom_round_supported(d->ctx, K) == 1;
-  bool mail = true;  // checks read through the context's mailbox while it has one
-  uint32_t prev_seq = 0;
-  uint64_t m = 0, checks = 0;
-  bool done = false, have_rows = false;
-  for (; !done; ++m) {
-    if (m >= cap) return fail(err, "dymu_dist_solve", "exchange-round cap reached",
-                              DYMU_ERR_NOT_CONVERGED);
-    const bool check = (m % kCheckEvery) == kCheckEvery - 1;
-    const int par = (int)(checks & 1);
-    int rc = fused ? dymu_dom_round(d->ctx, K, have_rows && s.lo ? p.r(0) : nullptr,
-                                    have_rows && s.hi ? p.r(1) : nullptr, p.tot(par), stream)
-                   : dymu_dom_run(d->ctx, K, stream);
-    if (rc) return fail(err, fused ? "dymu_dom_round" : "dymu_dom_run", dymu_last_error(d->ctx), rc);
-    if (s.lo || s.hi) {
-      DNCCL(err, ncclGroupStart());
-      if (s.lo) {
-        DNCCL(err, ncclSend(s.row(0), nx, ncclDouble, d->rank - 1, d->comm, st));
-        DNCCL(err, ncclRecv(p.r(0), nx, ncclDouble, d->rank - 1, d->comm, st));
-      }
-      if (s.hi) {
-        DNCCL(err, ncclSend(s.row(1), nx, ncclDouble, d->rank + 1, d->comm, st));
-        DNCCL(err, ncclRecv(p.r(1), nx, ncclDouble, d->rank + 1, d->comm, st));
-      }
-      DNCCL(err, ncclGroupEnd());
-    }
-    have_rows = true;
-    if (!fused) {
-      rc = dymu_dom_exchange(d->ctx, s.lo ? p.r(0) : nullptr, s.hi ? p.r(1) : nullptr, p.tot(par),
-                             stream);
-      if (rc) return fail(err, "dymu_dom_exchange", dymu_last_error(d->ctx), rc);
-    }
-    if (!check) continue;
-    DNCCL(err, ncclAllReduce(p.tot(par), p.sum(par), 1, ncclInt32, ncclSum, d->comm, st));
-    if (mail) {  // the next round's first pass posts the sum; read the previous check's
-      uint32_t seq = 0;
-      rc = dymu_dom_post(d->ctx, p.sum(par), &seq);
-      if (rc == DYMU_ERR_STATE && checks == 0) {
-        mail = false;
-      } else if (rc) {
-        return fail(err, "dymu_dom_post", dymu_last_error(d->ctx), rc);
-      } else {
-        if (checks >= 1) {
-          int32_t v = 0;
-          rc = dymu_dom_wait_post(d->ctx, prev_seq, dist_timeout_s(), &v, stream);
-          if (rc) return fail(err, "dymu_dom_wait_post", dymu_last_error(d->ctx), DYMU_ERR_RCCL);
-          done = v == 0;
-        }
-        prev_seq = seq;
-      }
-    }
-    if (!mail) {
-      DHIP(err, hipMemcpyAsync(d->h_sum + par, p.sum(par), sizeof(int32_t),
-                               hipMemcpyDeviceToHost, st));
-      DHIP(err, hipEventRecord(d->ev[par], st));
-      if (checks >= 1) {  // the previous check's global count; this one stays queued meanwhile
-        rc = wait_event(d->ev[par ^ 1], err);
-        if (rc) return rc;
-        done = d->h_sum[par ^ 1] == 0;
-      }
-    }
-    ++checks;
-  }
-  *rounds = m;
-  return DYMU_OK;
-}
-
-// Collective pre-flight: every rank learns whether every rank can solve, so a
-// rank-local argument error (an empty slab, a null buffer) fails all ranks
-// together instead of leaving the others blocked in their first exchange.
-int preflight(dymu_dist* d, bool ok, hipStream_t st) {
-  std::string* err = &d->last_error;
-  const Pipe& p = d->pipe;
-  d->h_sum[2] = ok ? 1 : 0;
-  DHIP(err, hipMemcpyAsync(p.flag(), d->h_sum + 2, sizeof(int32_t), hipMemcpyHostToDevice, st));
-  DNCCL(err, ncclAllReduce(p.flag(), p.flag(), 1, ncclInt32, ncclMin, d->comm, st));
-  DHIP(err, hipMemcpyAsync(d->h_sum + 2, p.flag(), sizeof(int32_t), hipMemcpyDeviceToHost, st));
-  DHIP(err, hipEventRecord(d->ev[0], st));
-  int rc = wait_event(d->ev[0], err);
-  if (rc) return rc;
-  if (d->h_sum[2] != 1)
-    return fail(err, "dymu_dist_solve", ok ? "another rank rejected its slab" : "invalid slab",
-                DYMU_ERR_ARG);
-  return DYMU_OK;
-}
-
-// After an error inside the collective sequence: abort the communicator (its
-// peers may be blocked in a send/recv this rank will never post), leave the
-// domain, and refuse further solves on this handle.
-int abort_comm(dymu_dist* d, int rc) {
-  if (d->comm) (void)ncclCommAbort(d->comm);
-  d->comm = nullptr;
-  d->aborted = true;
-  return rc;
-}
-
-}  // namespace
-
-extern "C" {
 
 int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t ld, uint32_t nx,
                     uint32_t ny, uint32_t goal_i, uint32_t goal_j, uint32_t K, void* stream,
                     dymu_stats* stats) {
   if (!d) return DYMU_ERR_ARG;
   std::string* err = &d->last_error;
-  if (d->aborted || !d->comm)
-    return fail(err, "dymu_dist_solve", "communicator aborted by an earlier error", DYMU_ERR_STATE);
+  if (d->aborted || !d->xp)
+    return fail(err, "dymu_dist_solve", "transport aborted by an earlier error", DYMU_ERR_STATE);
   if (K == 0) K = kDefaultK;
   DHIP(err, hipSetDevice(d->device));
-  if (pipe_alloc(&d->pipe, nx ? nx : 1) != DYMU_OK)
-    return abort_comm(d, fail(err, "pipe_alloc", "out of memory", DYMU_ERR_NOMEM));
-  // RCCL and the domain primitives share one stream: NULL = the context's
+  // the transport and the domain primitives share one stream: NULL = the context's
   if (!stream) stream = dymu_get_stream(d->ctx);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  Slab s;
+  std::vector<Local> L(1);
+  L[0].ctx = d->ctx;
+  L[0].rank = d->rank;
+  if (d->xp->alloc(L, nx ? nx : 1, err) != DYMU_OK)
+    return abort_dist(d, fail(err, "dymu_dist_solve", "receive rows: out of memory",
+                              DYMU_ERR_NOMEM));
   const bool ok = nx > 0 && ny > 0 && goal_i < nx && goal_j < ny &&
-                  make_slab(F_slab, T_buf, ld, nx, ny, goal_j, d->rank, d->world, &s) == DYMU_OK;
-  int rc = preflight(d, ok, st);
-  if (rc) return rc == DYMU_ERR_ARG ? rc : abort_comm(d, rc);
+                  make_slab(F_slab, T_buf, ld, nx, ny, goal_j, d->rank, d->world, &L[0].s) == DYMU_OK;
+  int rc = d->xp->preflight(ok, st, err);
+  if (rc) return rc == DYMU_ERR_ARG ? rc : abort_dist(d, rc);
+  rc = d->xp->connect(err);
+  if (rc) return abort_dist(d, rc);
+  const Slab& s = L[0].s;
   rc = dymu_dom_begin(d->ctx, &s.dom, s.goal_local >= 0 ? goal_i : 0, s.goal_local, stream);
-  if (rc) return abort_comm(d, fail(err, "dymu_dom_begin", dymu_last_error(d->ctx), rc));
+  if (rc) return abort_dist(d, fail(err, "dymu_dom_begin", dymu_last_error(d->ctx), rc));
   uint64_t rounds = 0;
-  rc = dist_rounds(d, s, nx, ny, K, stream, &rounds);
+  rc = run_rounds(L, *d->xp, d->res, nx, ny, K, st, err, &rounds);
   const int rf = dymu_dom_finish(d->ctx, stream, stats);
-  if (rc) return abort_comm(d, rc);
-  if (rf) return abort_comm(d, fail(err, "dymu_dom_finish", dymu_last_error(d->ctx), rf));
+  if (rc) return abort_dist(d, rc);
+  if (rf) return abort_dist(d, fail(err, "dymu_dom_finish", dymu_last_error(d->ctx), rf));
   if (stats) stats->rounds = rounds;
   return DYMU_OK;
 }
@@ -404,89 +804,29 @@ int dymu_vdist_solve(dymu_ctx* const* ctxs, int world, const double* const* F_sl
     return DYMU_ERR_ARG;
   if (K == 0) K = kDefaultK;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  std::vector<Slab> s(world);
+  std::vector<Local> L(world);
   for (int r = 0; r < world; ++r) {
     if (!ctxs[r]) return DYMU_ERR_ARG;
-    DCALL(make_slab(F_slabs[r], T_bufs[r], ld, nx, ny, goal_j, r, world, &s[r]));
+    L[r].ctx = ctxs[r];
+    L[r].rank = r;
+    DCALL(make_slab(F_slabs[r], T_bufs[r], ld, nx, ny, goal_j, r, world, &L[r].s));
   }
-  std::vector<Pipe> p(world);
-  int32_t* h_tot = nullptr;
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  struct Cleanup {
-    std::vector<Pipe>& p;
-    int32_t*& h;
-    hipEvent_t* e;
-    ~Cleanup() {
-      for (auto& q : p) pipe_free(&q);
-      if (h) (void)hipHostFree(h);
-      for (int k = 0; k < 2; ++k)
-        if (e[k]) (void)hipEventDestroy(e[k]);
-    }
-  } cleanup{p, h_tot, ev};
-  for (auto& q : p) DCALL(pipe_alloc(&q, nx));
-  DHIP(nullptr, hipHostMalloc(&h_tot, sizeof(int32_t) * 2 * world, hipHostMallocDefault));
-  for (auto& e : ev) DHIP(nullptr, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  VirtualTransport X;
+  LoopRes R;
+  std::string err;
+  DCALL(X.alloc(L, nx, &err));
+  DCALL(X.preflight(true, st, &err));
   for (int r = 0; r < world; ++r)
-    DCALL(dymu_dom_begin(ctxs[r], &s[r].dom, s[r].goal_local >= 0 ? goal_i : 0, s[r].goal_local,
-                         stream));
-  const uint64_t cap = max_rounds(nx, ny, K) + 2 * kCheckEvery;
-  uint64_t m = 0, checks = 0;
-  bool done = false;
-  int rc = DYMU_OK;
-  // the schedule of dymu_dist_solve with every rank's work serialised on one
-  // stream: device-to-device row copies for RCCL P2P, a host sum for the
-  // all-reduce
-  // fused rounds (kernel 5 slabs): as dist_rounds, the copied rows are merged by
-  // each rank's next round
-  bool fused = true;
-  for (int r = 0; r < world; ++r) fused = fused && dymu_dom_round_supported(ctxs[r], K) == 1;
-  bool have_rows = false;
-  for (; !done && rc == DYMU_OK; ++m) {
-    if (m >= cap) {
-      rc = DYMU_ERR_NOT_CONVERGED;
-      break;
-    }
-    const bool check = (m % kCheckEvery) == kCheckEvery - 1;
-    const int par = (int)(checks & 1);
-    for (int r = 0; r < world && rc == DYMU_OK; ++r)
-      rc = fused ? dymu_dom_round(ctxs[r], K, have_rows && s[r].lo ? p[r].r(0) : nullptr,
-                                  have_rows && s[r].hi ? p[r].r(1) : nullptr, p[r].tot(par), stream)
-                 : dymu_dom_run(ctxs[r], K, stream);
-    if (rc) break;
-    for (int r = 0; r < world; ++r) {  // rank r-1's last row / rank r+1's first row
-      if (s[r].lo)
-        DHIP(nullptr, hipMemcpyAsync(p[r].r(0), s[r - 1].row(1), sizeof(double) * nx,
-                                     hipMemcpyDeviceToDevice, st));
-      if (s[r].hi)
-        DHIP(nullptr, hipMemcpyAsync(p[r].r(1), s[r + 1].row(0), sizeof(double) * nx,
-                                     hipMemcpyDeviceToDevice, st));
-    }
-    have_rows = true;
-    for (int r = 0; r < world && rc == DYMU_OK; ++r) {
-      if (!fused)
-        rc = dymu_dom_exchange(ctxs[r], s[r].lo ? p[r].r(0) : nullptr,
-                               s[r].hi ? p[r].r(1) : nullptr, p[r].tot(par), stream);
-      if (rc == DYMU_OK && check &&
-          hipMemcpyAsync(h_tot + par * world + r, p[r].tot(par), sizeof(int32_t),
-                         hipMemcpyDeviceToHost, st) != hipSuccess)
-        rc = DYMU_ERR_HIP;
-    }
-    if (rc) break;
-    if (!check) continue;
-    DHIP(nullptr, hipEventRecord(ev[par], st));
-    if (checks >= 1) {
-      DHIP(nullptr, hipEventSynchronize(ev[par ^ 1]));
-      int64_t tot = 0;
-      for (int r = 0; r < world; ++r) tot += h_tot[(par ^ 1) * world + r];
-      done = tot == 0;
-    }
-    ++checks;
-  }
+    DCALL(dymu_dom_begin(ctxs[r], &L[r].s.dom, L[r].s.goal_local >= 0 ? goal_i : 0,
+                         L[r].s.goal_local, stream));
+  uint64_t rounds = 0;
+  int rc = run_rounds(L, X, R, nx, ny, K, st, &err, &rounds);
+  if (rc && std::getenv("DYMU_DIST_DEBUG")) std::fprintf(stderr, "dymu_vdist_solve: %s\n", err.c_str());
   for (int r = 0; r < world; ++r) {
     dymu_stats tmp;
     const int rf = dymu_dom_finish(ctxs[r], stream, stats ? &stats[r] : &tmp);
     if (rc == DYMU_OK) rc = rf;
-    if (stats) stats[r].rounds = m;
+    if (stats) stats[r].rounds = rounds;
   }
   return rc;
 }

@@ -1,14 +1,17 @@
 """Row-slab sharded solve driven natively (libdymu_dist.so, include/dymu_dist.h).
 
 The exchange loop of dymu.sharded.SlabSolver, moved into C++ on the engine's
-stream: K passes -> grouped ncclSend/ncclRecv of the boundary rows with rank±1
-(RCCL over xGMI) -> min-merge into the ghost rows -> ncclAllReduce of the queued
-tile count, read back one round late so the host never drains the device queue.
+stream: K passes (the first merges the rows received after the previous round
+into the ghost rows) -> the boundary rows to rank±1 -> every 4th round a
+reduction of the queued tile count, read one check late through the engine's
+mailbox so the host never drains the device queue.  One loop, three transports:
+  "rccl"  grouped ncclSend/ncclRecv over xGMI + ncclAllReduce (one GPU per rank)
+  "ipc"   rows pushed into the neighbours' hipIpc-mapped receive rows, counts
+          reduced through a /dev/shm board (ranks of one node, may share a GPU)
+  vdist_solve: every rank in this process (device-to-device copies).
 
-torch.distributed only carries the control plane here (the 128-byte RCCL
-communicator id, barriers, timing); the data path is the library's own RCCL
-communicator.  `VirtualWorld` runs the same loop with N slabs in one process on
-one GPU (device-to-device copies instead of RCCL) for the tests.
+torch.distributed only carries the control plane here (the 128-byte id,
+barriers, timing); the data path is the library's own transport.
 
 Reference: computeEntireTotalCostMap's propagation loop
 (src/DyMu_GlobalPathPlanning.cpp:443-468), distributed as SURVEY.md s8(e).
@@ -32,6 +35,9 @@ DIST_SYMBOLS = {
     "dymu_vdist_solve": (_i32, [ctypes.POINTER(_vp), _i32, ctypes.POINTER(_vp),
                                 ctypes.POINTER(_vp), _u64, _u32, _u32, _u32, _u32, _u32, _vp,
                                 ctypes.POINTER(DymuStats)]),
+    "dymu_dist_ipc_unique_id": (_i32, [ctypes.c_char_p]),
+    "dymu_dist_create_ipc": (_i32, [ctypes.POINTER(_vp), _vp, _i32, ctypes.c_char_p, _i32, _i32]),
+    "dymu_dist_transport": (_i32, [_vp]),
     "dymu_dist_last_error": (ctypes.c_char_p, [_vp]),
     "dymu_dist_comm_count": (_i32, [_vp, ctypes.POINTER(ctypes.c_int)]),
 }
@@ -55,29 +61,38 @@ def load_dist() -> ctypes.CDLL:
     return _dl
 
 
-def unique_id() -> bytes:
-    """A fresh RCCL communicator id (call on rank 0, broadcast the bytes)."""
+TRANSPORTS = ("rccl", "ipc")
+
+
+def unique_id(transport: str = "rccl") -> bytes:
+    """A fresh transport id (call on rank 0, broadcast the bytes): the RCCL
+    communicator id, or the IPC board's shared-memory name."""
     buf = ctypes.create_string_buffer(ID_BYTES)
-    _check(load_dist().dymu_dist_unique_id(buf))
+    lib = load_dist()
+    fn = lib.dymu_dist_ipc_unique_id if transport == "ipc" else lib.dymu_dist_unique_id
+    _check(fn(buf))
     return buf.raw
 
 
 class DistSolver:
     """One rank of the native sharded solver.  Collective construction."""
 
-    def __init__(self, engine, device: int, uid: bytes, rank: int, world: int):
-        assert len(uid) == ID_BYTES
+    def __init__(self, engine, device: int, uid: bytes, rank: int, world: int,
+                 transport: str = "rccl"):
+        assert len(uid) == ID_BYTES and transport in TRANSPORTS
         self._lib = load_dist()
         self.eng = engine
         self.rank, self.world = rank, world
+        self.transport = transport
         self.h = _vp()
-        rc = self._lib.dymu_dist_create(ctypes.byref(self.h), engine.ctx, device, uid, rank,
-                                        world)
+        create = (self._lib.dymu_dist_create_ipc if transport == "ipc"
+                  else self._lib.dymu_dist_create)
+        rc = create(ctypes.byref(self.h), engine.ctx, device, uid, rank, world)
         if rc != 0:
-            raise DymuError(rc, "dymu_dist_create (RCCL communicator)")
+            raise DymuError(rc, f"dymu_dist_create ({transport} transport)")
 
     def comm_count(self) -> int:
-        """Ranks in the RCCL communicator (ncclCommCount)."""
+        """Ranks the transport sees (ncclCommCount, or the IPC board's)."""
         n = ctypes.c_int(0)
         rc = self._lib.dymu_dist_comm_count(self.h, ctypes.byref(n))
         if rc != 0:
