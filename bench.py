@@ -56,9 +56,11 @@ def parse():
                     help="no per-launch events (roofline reported as null)")
     ap.add_argument("--backend", default="nccl",
                     help="N>1 only: 'nccl' (RCCL over xGMI) or 'gloo' (host-staged rehearsal)")
-    ap.add_argument("--exchange", default="native", choices=["native", "python"],
+    ap.add_argument("--exchange", default="native", choices=["native", "ipc", "python"],
                     help="N>1: 'native' = C++ exchange loop with its own RCCL communicator "
-                         "(libdymu_dist); 'python' = dymu.sharded over torch.distributed")
+                         "(libdymu_dist); 'ipc' = the same loop over hipIpc-mapped rows and a "
+                         "shared-memory board (N ranks may share one GPU); 'python' = "
+                         "dymu.sharded over torch.distributed")
     ap.add_argument("--passes-per-exchange", type=int, default=0,
                     help="passes per exchange round (0: 4 for the native loop, 16 for the "
                          "python loop; tools/vdist_rehearsal.py)")
@@ -361,8 +363,9 @@ def main():
             "grid": N,
             "parallelism": ("single" if world == 1 and not args.sharded else
                             f"row-slab x{world} ("
-                            + ("RCCL, native C++ loop" if args.exchange == "native"
-                               else f"{args.backend}, torch.distributed loop") + ")"),
+                            + {"native": "RCCL, native C++ loop",
+                               "ipc": "hipIpc rows + shared-memory board, native C++ loop"}
+                            .get(args.exchange, f"{args.backend}, torch.distributed loop") + ")"),
             "exchange_rounds_per_solve": tot.get("rounds", 0) / K,
             "passes_per_solve": tot["passes"] / K,
             # a tile is first relaxed one pass after its 4-neighbour that reaches it,
@@ -380,6 +383,8 @@ def main():
         "roofline": roof,
         "cpu_baseline": None,
     }
+    if tot.get("parity") is not None:  # the sharded run's self-check (bench_sharded.self_check)
+        line["parity"] = tot["parity"]
     if args.fake_cpu:
         line["data"] = "synthetic; --fake-cpu plumbing rehearsal (numpy engine, not a GPU number)"
     if world == 1 and not args.no_planner and not args.fake_cpu and not args.sharded:
@@ -397,6 +402,8 @@ def main():
         line["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.obst)
         line["cpu_reference_algorithm"] = cpu_reference_algorithm(1024, args.obst)
     print(json.dumps(line), flush=True)
+    if line.get("parity") is not None and not line["parity"]["ok"]:
+        sys.exit(f"bench: the stitched map failed its self-check: {line['parity']}")
 
 
 if __name__ == "__main__":

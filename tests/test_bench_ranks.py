@@ -41,6 +41,10 @@ def test_bench_gpus2_spawns_two_ranks(oracle, tmp_path):
     assert [s[0] for s in slabs] == [0, 1]
     assert slabs[0][1] == 0 and slabs[0][1] + slabs[0][2] == slabs[1][1]
     assert slabs[1][1] + slabs[1][2] == n
+    # the run's own check of its stitched map (bench_sharded.self_check)
+    par = rec["parity"]
+    assert par["ok"] and par["residual"] <= 1e-12 and par["sum_rel"] <= 1e-12
+    assert par["finite_cells"] == par["finite_cells_single"] and par["ghost_max_abs_diff"] == 0
     T = np.empty((n, n))
     files = glob.glob(str(tmp_path / "T_rank*_row*.npy"))
     assert len(files) == 2

@@ -126,6 +126,27 @@ def test_fixed_point_detects_errors(dymu):
         check_fixed_point(T, F, g)
 
 
+def test_parity_16384_config3_oracle(dymu, oracle):
+    """BASELINE config 3 -- the headline grid, 16384^2, 2% obstacles, goal at the
+    centre -- whole-map parity with the oracle FMM (reference pop order, ~50 s of
+    one host core): identical +inf mask, every finite cell within 1e-12."""
+    import torch
+
+    N = 16384
+    F, T, g, st = _solve_on_device(dymu, N)
+    Th = T.cpu().numpy()
+    del T
+    assert np.array_equal(F.cpu().numpy()[:64], oracle.synth_speed(
+        N, 64, seed=1, obst_frac=0.02, obst_seed=3, goal=g))  # the oracle's input
+    Fh = F.cpu().numpy()
+    del F
+    torch.cuda.empty_cache()
+    Tref, _ = oracle.fmm(Fh, g)
+    del Fh
+    assert_parity(Th, Tref)
+    assert st["kernel"] == 5
+
+
 def test_parity_8192_oracle(dymu, oracle):
     """Whole-map parity with the oracle FMM at 8192^2 (device synth, device solve)."""
     F, T, g, _ = _solve_on_device(dymu, 8192)

@@ -192,6 +192,40 @@ def test_early_exit_random_vs_oracle(dymu, oracle, seed):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("inputs", ["splitmix", "mt19937"])
+def test_config1_exact_call(dymu, oracle, inputs):
+    """BASELINE config 1 as the caller makes it: a 512^2
+    setCostMap grid without obstacles, goal (256, 256), computeTotalCostMap from
+    the start (102, 128) (:364-408) -- the whole getTotalCostMatrix (CLOSED values,
+    the band's tentative values, -1 never reached) against the oracle's exact
+    early exit -- then computeEntireTotalCostMap (:443-468) on the same planner
+    against the oracle's full FMM.  Both generators: the counter-based U(1,5) of
+    the synthetic configs and the reference-run KAT input (mt19937_64(1))."""
+    N, g, s = 512, (256, 256), (102, 128)
+    if inputs == "splitmix":
+        F = oracle.synth_speed(N, N, seed=1, obst_frac=0.0, obst_seed=3, goal=g)
+    else:
+        F = oracle.mt_uniform(N * N).reshape(N, N)
+    p = dymu.Planner()
+    p.initGlobalLayer(1.0, 0.5, N, N)
+    p.setCostMap(F)
+    assert p.setGoal(g)
+    Tt, rc, _ = oracle.fmm(F, g, start=s, want_closed=True)
+    assert rc == 1  # the reference returns true: the band is not empty at the exit
+    assert p.computeTotalCostMap(s)
+    M = p.getTotalCostMatrix()
+    _early_matches(M, Tt)
+    assert 0 < p.lastBandSize() and (M == -1.0).any()  # stopped before the map was covered
+    assert p.computeEntireTotalCostMap()
+    Tref, _ = oracle.fmm(F, g)
+    M = p.getTotalCostMatrix()
+    assert np.array_equal(M == -1.0, np.isinf(Tref))
+    assert (np.abs(M - Tref) / np.maximum(1, Tref)).max() <= RTOL
+    if inputs == "mt19937":  # the reference-run KAT (SURVEY s8(c)) through the class surface
+        assert f"{M.sum():.10e}" == "1.3467278246e+08"
+
+
+@pytest.mark.gpu
 def test_early_exit_false_returns(dymu, oracle):
     """The reference returns false when the band is empty at exit (:399-403):
     a start enclosed by obstacles (unreachable), and a start whose neighbourhood
