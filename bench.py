@@ -66,6 +66,8 @@ def parse():
                          "python loop; tools/vdist_rehearsal.py)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the row-slab path even at N=1 (exercises the RCCL code path)")
+    ap.add_argument("--no-variants", action="store_true",
+                    help="skip the exact-sqrt / deterministic re-runs of the headline solve")
     ap.add_argument("--no-planner", action="store_true",
                     help="skip the class-surface leg (computeEntireTotalCostMap through "
                          "libdymu_planner.so)")
@@ -196,9 +198,27 @@ def run_single(args):
     eng.set_profiling(False)
     T = np.empty(2)
     eng.d2h(T, dT)  # touch the result
+    # the same solve with the arithmetic / schedule options the headline leaves off
+    # (DESIGN.md s4): the correctly rounded sweep sqrt (every update bit-identical
+    # to the reference formula, :531-535) and the bit-reproducible schedule
+    variants = {}
+    if not args.no_variants:
+        for name, kw in (("exact_sqrt", dict(exact_sqrt=1)),
+                         ("deterministic", dict(deterministic=1))):
+            ev = dymu.Engine(device=int(os.environ.get("LOCAL_RANK", "0")), **kw)
+            ev.solve_device(dF, dT, N, N, N, g[0], g[1])  # warmup
+            n_v = max(2, min(args.steps, 5))
+            t1 = time.perf_counter()
+            for _ in range(n_v):
+                sv = ev.solve_device(dF, dT, N, N, N, g[0], g[1])
+            ms = (time.perf_counter() - t1) / n_v * 1e3
+            variants[name] = {"ms_per_step": round(ms, 3), "value": round(N * N / ms / 1e3, 3),
+                              "passes": sv["passes"], "steps": n_v}
+            ev.close()
     eng.free(dF)
     eng.free(dT)
     eng.close()
+    tot["variants"] = variants
     return dt, tot, kern_ms, kern_n, st
 
 
@@ -361,6 +381,12 @@ def main():
             "workload": f"config 3: {N}x{N} grid, {world}x MI355X, splitmix64 U(1,5) speed, "
                         f"{args.obst:.0%} iid obstacles, goal centre, full solve",
             "grid": N,
+            # what the headline computes in (DESIGN.md s4 "Sweep sqrt", s3 tolerance)
+            "arith": ("fp64, correctly rounded sweep sqrt (DYMU_EXACT_SQRT=1)" if _EXACT else
+                      "fp64, approx sweep sqrt (one Goldschmidt step, <= 36 ulp on the "
+                      "two-sided candidate; solve error vs the reference FMM <= 6e-15 rel)"),
+            "schedule": "default (sweep deadline + first-insertion histogram: last ulps vary "
+                        "run to run)",
             "parallelism": ("single" if world == 1 and not args.sharded else
                             f"row-slab x{world} ("
                             + {"native": "RCCL, native C++ loop",
@@ -383,6 +409,8 @@ def main():
         "roofline": roof,
         "cpu_baseline": None,
     }
+    if tot.get("variants"):
+        line["variants"] = tot["variants"]
     if tot.get("parity") is not None:  # the sharded run's self-check (bench_sharded.self_check)
         line["parity"] = tot["parity"]
     if args.fake_cpu:

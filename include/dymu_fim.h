@@ -300,6 +300,19 @@ int dymu_pack_speed(dymu_ctx* ctx, uint32_t nx, uint32_t ny, uint64_t ld, double
  * the event overhead out of the timed region (period 1 costs ~4 us/launch). */
 int dymu_set_profiling(dymu_ctx* ctx, int period);
 
+/* Per-pass statistics of kernel 5 (diagnostics; off by default, costs a few
+ * atomics per workgroup per pass when on): enable, then after a solve read one
+ * record of DYMU_PASS_STAT_WORDS words per pass (the first min(launches, 16384)
+ * passes; *n = their number):
+ *   [0] listed entries   [1] tiles relaxed    [2] colour-deferred entries
+ *   [3] key-deferred entries (tile loaded, key above the pass threshold)
+ *   [4] visits stopped by the sweep cap   [5] ... by the pass deadline
+ *   [6] largest / [9] smallest Manhattan tile distance from the goal's tile relaxed
+ *   [7] in-tile sweeps   [8] threshold bin   [10] entries appended to the next list */
+#define DYMU_PASS_STAT_WORDS 12
+int dymu_set_pass_stats(dymu_ctx* ctx, int enable);
+int dymu_last_pass_stats(dymu_ctx* ctx, uint32_t* out, uint64_t cap_passes, uint64_t* n);
+
 /* Summed kernel time (ms, HIP events on the launch stream) of the most recent
  * solve's SAMPLED pass launches and their count: the mean launch duration is
  * pass_ms_total / n_pass_launches -- the bench's roofline source. */

@@ -113,6 +113,11 @@ struct dymu_ctx {
     size_t prof_used = 0;
   } dom;
 
+  // per-pass statistics (kernel 5; dymu_set_pass_stats): kPassStatCap records of
+  // kShards x kPsWords words, pass p at p % kPassStatCap
+  int pass_stats = 0;
+  uint32_t* d_pstat = nullptr;
+
   // profiling
   int profiling = 0;
   std::vector<hipEvent_t> prof_ev;
@@ -330,6 +335,13 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   a.shard_cap = ntiles;
   a.tile_epoch = c->d_tile_epoch;
   a.stats = c->d_stats;
+  a.goal_tx = gj >= 0 ? (int)(gi / TWd) : 0;
+  a.goal_ty = gj >= 0 ? (int)(gj / THd) : 0;
+  if (c->pass_stats && D.variant == 5) {
+    const size_t bytes = sizeof(uint32_t) * (size_t)kPassStatCap * kShards * kPsWords;
+    if (!c->d_pstat) HIPC(c, hipMalloc(&c->d_pstat, bytes));
+    HIPC(c, hipMemsetAsync(c->d_pstat, 0, bytes, st));
+  }
   // resident workgroups per CU at the kernel's register / LDS budget
   D.blocks = c->opts.grid_blocks > 0 ? c->opts.grid_blocks
                                       : c->cu_count * c->occupancy[D.variant];
@@ -379,6 +391,9 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st, uint32_t report_seq = 0)
       c->arm_seq = 0;
       c->arm_src = nullptr;
     }
+    a.pstat = (c->pass_stats && D.variant == 5 && c->d_pstat)
+                  ? c->d_pstat + (p % kPassStatCap) * (uint64_t)kShards * kPsWords
+                  : nullptr;
     const bool tr = is_prio(D.variant) && c->prio_trace >= 0 && p == (uint64_t)c->prio_trace;
     if (tr) {
       if (!c->d_trace)
@@ -980,6 +995,7 @@ int dymu_destroy(dymu_ctx* c) {
   if (c->d_hist) (void)hipFree(c->d_hist);
   if (c->d_prio) (void)hipFree(c->d_prio);
   if (c->d_trace) (void)hipFree(c->d_trace);
+  if (c->d_pstat) (void)hipFree(c->d_pstat);
   if (c->d_lut) (void)hipFree(c->d_lut);
   if (c->d_scratch) (void)hipFree(c->d_scratch);
   if (c->d_xchg) (void)hipFree(c->d_xchg);
@@ -1363,6 +1379,38 @@ int dymu_pack_speed(dymu_ctx* c, uint32_t nx, uint32_t ny, uint64_t ld, double g
   a.st = cost_state(st);
   a.F = dF;
   HIPC(c, dymu::launch_pack_speed(a, pick_stream(c, stream)));
+  return DYMU_OK;
+}
+
+int dymu_set_pass_stats(dymu_ctx* c, int enable) {
+  if (!c) return DYMU_ERR_ARG;
+  c->pass_stats = enable != 0;
+  return DYMU_OK;
+}
+
+int dymu_last_pass_stats(dymu_ctx* c, uint32_t* out, uint64_t cap, uint64_t* n) {
+  if (!c || !n || (cap && !out)) return DYMU_ERR_ARG;
+  *n = 0;
+  if (!c->d_pstat || !c->pass_stats) return DYMU_ERR_STATE;
+  HIPC(c, hipSetDevice(c->device));
+  const uint64_t passes = std::min<uint64_t>(c->last_launches, kPassStatCap);
+  *n = passes;
+  const uint64_t m = std::min(passes, cap);
+  if (!m) return DYMU_OK;
+  std::vector<uint32_t> h((size_t)m * kShards * kPsWords);
+  HIPC(c, hipMemcpy(h.data(), c->d_pstat, sizeof(uint32_t) * h.size(), hipMemcpyDeviceToHost));
+  for (uint64_t p = 0; p < m; ++p) {
+    uint32_t* o = out + p * kPsWords;
+    std::memset(o, 0, sizeof(uint32_t) * kPsWords);
+    for (int q = 0; q < kShards; ++q) {
+      const uint32_t* r = &h[(p * kShards + q) * kPsWords];
+      for (int w = 0; w < kPsWords; ++w) {
+        if (w == kPsRadiusMax || w == kPsRadiusMin) o[w] = std::max(o[w], r[w]);
+        else o[w] += r[w];
+      }
+    }
+    o[kPsRadiusMin] = o[kPsRadiusMin] ? ~o[kPsRadiusMin] : 0u;  // stored as ~radius
+  }
   return DYMU_OK;
 }
 

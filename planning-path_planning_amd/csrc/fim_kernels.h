@@ -81,7 +81,29 @@ struct PassArgs {
   uint32_t* tot_save;       // block 0 stores the pass's count here ...
   const uint32_t* tot_prev;  // ... and a later pass stores *tot_prev + its count
   int32_t* tot_out;          //     into *tot_out (the round's termination count)
+  // ---- kernel 5, per-pass statistics (dymu_set_pass_stats; off = null) ----
+  // this pass's record: kShards rows of kPsWords words (PassStat), one row per
+  // workgroup shard, summed (max / min for the radii) by the host
+  uint32_t* pstat;
+  int goal_tx, goal_ty;  // the goal's tile (radius = Manhattan tile distance from it)
 };
+
+// per-pass statistics words (kernel 5)
+enum PassStat : int {
+  kPsActive = 0,    // listed entries (block 0)
+  kPsVisited = 1,   // tiles relaxed
+  kPsColour = 2,    // entries deferred by the checkerboard colour (no tile load)
+  kPsKey = 3,       // entries deferred by the key threshold (tile loaded, then skipped)
+  kPsCapped = 4,    // visits stopped by the sweep cap (re-queued)
+  kPsDeadline = 5,  // visits stopped by the pass deadline (re-queued)
+  kPsRadiusMax = 6, // largest tile radius relaxed (atomicMax; 0 = none or the goal tile)
+  kPsSweeps = 7,    // in-tile sweeps
+  kPsBstar = 8,     // threshold bin (block 0)
+  kPsRadiusMin = 9, // ~smallest tile radius relaxed (atomicMin of ~r... stored as 0xFFFFFFFF - r)
+  kPsEnqueued = 10, // entries appended to the next list (activations + deferrals)
+  kPsWords = 12
+};
+constexpr uint32_t kPassStatCap = 16384;  // passes kept (a ring; pass p at p % cap)
 
 constexpr int kBins = 64;  // v4/v5 key histogram bins
 constexpr int kTracePts = 10;

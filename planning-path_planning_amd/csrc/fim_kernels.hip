@@ -1089,6 +1089,8 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   __shared__ unsigned long long s_visits, s_sweeps, s_minout, s_defer;
   __shared__ unsigned long long s_ek[WPB][4];
   __shared__ double s_img[WPB][IMG];
+  __shared__ uint32_t s_ps[4];  // pass statistics: colour, capped, deadline, max radius
+  __shared__ uint32_t s_psmin;  // ~min radius
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1131,6 +1133,8 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       s_sweeps = 0;
       s_defer = 0;
       s_minout = kInfBits;
+      s_ps[0] = s_ps[1] = s_ps[2] = s_ps[3] = 0u;
+      s_psmin = 0u;
     }
   }
   s_hout[tid & (kBins - 1)] = 0u;
@@ -1147,6 +1151,10 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       if (n_active > 0) {
         atomicAdd(&a.stats[kStatPasses], 1ull);
         atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
+      }
+      if (a.pstat) {
+        a.pstat[kPsActive] = n_active;
+        a.pstat[kPsBstar] = (uint32_t)bstar;
       }
       report_pending(a, n_active);
       if (a.tot_save) *a.tot_save = n_active;
@@ -1170,6 +1178,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   };
 
   unsigned long long my_visits = 0, my_sweeps = 0, my_defer = 0;
+  uint32_t my_cd = 0, my_cap = 0, my_dl = 0, my_rmax = 0, my_rmin = ~0u;  // a.pstat only
   double* img = s_img[wv];
   unsigned long long* ek = s_ek[wv];
   const uint32_t chunk = (n_active + gridDim.x - 1) / gridDim.x;
@@ -1194,6 +1203,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
         enqueue(tile, k0);
       }
       ++my_defer;
+      if (a.pstat) ++my_cd;
       continue;
     }
     const unsigned long long kb = a.key_in[tile];
@@ -1217,6 +1227,15 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     my_visits += 1;
     my_sweeps += (unsigned long long)sweeps;
     const bool cap = __any(capped);
+    if (a.pstat) {
+      if (cap) {
+        if (sweeps >= a.max_inner) ++my_cap;
+        else ++my_dl;
+      }
+      const uint32_t rad = (uint32_t)(abs(tx - a.goal_tx) + abs(ty - a.goal_ty));
+      my_rmax = rad > my_rmax ? rad : my_rmax;
+      my_rmin = rad < my_rmin ? rad : my_rmin;
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     bool want = false;
@@ -1278,6 +1297,13 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     atomicAdd(&s_visits, my_visits);
     atomicAdd(&s_sweeps, my_sweeps);
     atomicAdd(&s_defer, my_defer);
+    if (a.pstat) {
+      atomicAdd(&s_ps[0], my_cd);
+      atomicAdd(&s_ps[1], my_cap);
+      atomicAdd(&s_ps[2], my_dl);
+      atomicMax(&s_ps[3], my_rmax);
+      if (my_visits) atomicMax(&s_psmin, ~my_rmin);
+    }
   }
   __syncthreads();
   const uint32_t nq = s_nq < QCAP ? s_nq : QCAP;
@@ -1289,6 +1315,18 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       atomicAdd(&st[kStatVisits], s_visits);
       atomicAdd(&st[kStatSweeps], s_sweeps);
       if (s_defer) atomicAdd(&st[kStatDeferred], s_defer);
+    }
+    if (a.pstat) {  // one row per shard: 16 workgroups per address
+      uint32_t* ps = a.pstat + (uint64_t)shard * kPsWords;
+      atomicAdd(&ps[kPsVisited], (uint32_t)s_visits);
+      atomicAdd(&ps[kPsColour], s_ps[0]);
+      atomicAdd(&ps[kPsKey], (uint32_t)s_defer - s_ps[0]);
+      atomicAdd(&ps[kPsCapped], s_ps[1]);
+      atomicAdd(&ps[kPsDeadline], s_ps[2]);
+      atomicMax(&ps[kPsRadiusMax], s_ps[3]);
+      atomicAdd(&ps[kPsSweeps], (uint32_t)s_sweeps);
+      atomicMax(&ps[kPsRadiusMin], s_psmin);
+      atomicAdd(&ps[kPsEnqueued], s_nq);
     }
   }
   if (tid < kBins && s_hout[tid]) atomicAdd(&a.hist_out[shard * kBins + tid], s_hout[tid]);

@@ -112,6 +112,8 @@ FIM_SYMBOLS = {
     "dymu_memcpy_d2h": (_i32, [_vp, _vp, _vp, ctypes.c_size_t]),
     "dymu_memcpy_h2d": (_i32, [_vp, _vp, _vp, ctypes.c_size_t]),
     "dymu_set_profiling": (_i32, [_vp, _i32]),
+    "dymu_set_pass_stats": (_i32, [_vp, _i32]),
+    "dymu_last_pass_stats": (_i32, [_vp, _vp, _u64, ctypes.POINTER(_u64)]),
     "dymu_eikonal_batch": (_i32, [_vp, _vp, _vp, _vp, _vp, _u64, _i32]),
     "dymu_slab_rows": (_i32, [_u32, _u32, _u32, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
     "dymu_dom_begin": (_i32, [_vp, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, _vp]),
@@ -385,6 +387,22 @@ class Engine:
     def set_profiling(self, period):
         """Time every `period`-th pass launch (True = every launch, 0/False = off)."""
         _check(self._lib.dymu_set_profiling(self.ctx, int(period)), self.ctx)
+
+    PASS_STAT_FIELDS = ("listed", "visited", "colour_deferred", "key_deferred", "capped",
+                        "deadline", "radius_max", "sweeps", "bstar", "radius_min", "enqueued")
+
+    def set_pass_stats(self, on=True):
+        """Kernel 5 per-pass statistics for the next solves (diagnostics)."""
+        _check(self._lib.dymu_set_pass_stats(self.ctx, int(bool(on))), self.ctx)
+
+    def last_pass_stats(self) -> np.ndarray:
+        """(passes, 12) uint32 records of the last solve (fields: PASS_STAT_FIELDS)."""
+        n = _u64()
+        cap = 1 << 14
+        out = np.zeros((cap, 12), dtype=np.uint32)
+        _check(self._lib.dymu_last_pass_stats(self.ctx, out.ctypes.data, cap, ctypes.byref(n)),
+               self.ctx)
+        return out[:n.value].copy()
 
     def last_pass_timing(self):
         ms, n = ctypes.c_double(), ctypes.c_uint64()
