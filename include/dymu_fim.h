@@ -238,8 +238,13 @@ int dymu_host_unregister(dymu_ctx* ctx, void* p);
  * the old speed to that of the new one without a cold solve: cells whose old
  * T is below theta = min(old T over the window and its 1-cell ring) provably
  * keep their value; the rest is reset and re-propagated from the boundary of
- * the kept region.  Increases and decreases are both handled;
- * the result is the fixed point a cold dymu_solve of the new speed reaches.
+ * the kept region.  With DYMU_RAISE=1 a raise front instead
+ * sets to +inf exactly the cells whose converged value is no longer supported
+ * under the new speed (the window's dependency cone; cells supported within
+ * 1e-13 relative keep their value) and the FIM re-propagates the cone from its
+ * boundary -- exact and smaller, but slower on config 5.
+ * Increases and decreases are both handled; the result is the fixed point a
+ * cold dymu_solve of the new speed reaches.
  * The window is clipped to the grid. */
 int dymu_resolve_window_device(dymu_ctx* ctx, const double* dF, double* dT, uint32_t nx,
                                uint32_t ny, uint64_t ld, uint32_t goal_i, uint32_t goal_j,
@@ -256,6 +261,10 @@ int dymu_update_window_device(dymu_ctx* ctx, const double* dF, double* dT, uint3
                               uint32_t ny, uint64_t ld, uint32_t goal_i, uint32_t goal_j,
                               uint32_t i0, uint32_t j0, uint32_t w, uint32_t h, int decrease_only,
                               void* stream, dymu_stats* stats);
+/* What the last windowed update did before its re-solve: out[0] raise passes,
+ * out[1] tiles visited by them, out[2] cells invalidated (the dependency cone of
+ * the window's speed increases; 0s for decrease-only updates), out[3] reserved. */
+int dymu_last_update_stats(dymu_ctx* ctx, uint64_t out[4]);
 /* Host-buffer form: requires that the previous dymu_solve / dymu_resolve_window
  * on this context solved the same grid size and goal (DYMU_ERR_STATE otherwise);
  * only the window of F is uploaded, the whole new T is written to T_out. */

@@ -117,6 +117,12 @@ struct dymu_ctx {
   // kShards x kPsWords words, pass p at p % kPassStatCap
   int pass_stats = 0;
   uint32_t* d_pstat = nullptr;
+  // windowed updates with increases: theta reset (0, default) or the raise front (1,
+  // DYMU_RAISE=1: exact dependency cone, measured slower on config 5 -- 9.5 vs 4.1 ms
+  // at 4096^2, profiles/r03/configs_4096_r03c.json); the last
+  // update's raise passes, raise visits, cells invalidated
+  int raise = 0;
+  uint64_t last_update[4] = {0, 0, 0, 0};
 
   // profiling
   int profiling = 0;
@@ -822,10 +828,18 @@ int solve_until_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uin
 // the previous speed, dF the new speed, which differs only inside the window.
 // decrease_only: the caller guarantees no speed in the window went up; then the
 // old map is kept whole and only the window's tiles are seeded (k_seed_window).
+// Otherwise (c->raise, default) the raise front invalidates the dependency cone of
+// the window (k_raise passes) and the FIM re-solves the cone from
+// its boundary plus the window when c->raise (DYMU_RAISE=1); by default every cell
+// at or above theta is reset instead (k_reset_seed): a larger region, but one the
+// FIM fills in key order from a single level set, where the cone is filled from
+// its whole lateral boundary -- 4.1 ms / 192 K visits vs 9.5 ms (252 raise passes +
+// 163 K visits) for config 5 at 4096^2.
 int resolve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
                  uint32_t gi, uint32_t gj, uint32_t i0, uint32_t j0, uint32_t w, uint32_t h,
                  hipStream_t st, dymu_stats* stats, bool decrease_only = false) {
   if (gi >= nx || gj >= ny || w == 0 || h == 0 || i0 >= nx || j0 >= ny) return DYMU_ERR_ARG;
+  std::memset(c->last_update, 0, sizeof c->last_update);
   int rc = dom_begin(c, dF, dT, nx, ny, ld, 0, 0, -1, -1, st, /*cold=*/false);
   if (rc) return rc;
   auto& D = c->dom;
@@ -846,10 +860,74 @@ int resolve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_
   u.gi = gi;
   u.gj = gj;
   u.theta_bits = theta;
-  u.list = D.lists[0];
-  u.counts = D.counts[0];
   u.shard_cap = D.ntiles;
   u.tile_epoch = c->d_tile_epoch;
+  const bool raise = !decrease_only && c->raise;
+  if (raise) {
+    // the raise passes use the domain's lists and epochs (plain FIM lists, 16x16 tiles)
+    const uint32_t ntx16 = (nx + 15) / 16, nty16 = (ny + 15) / 16;
+    u.list = D.lists[0];
+    u.counts = D.counts[0];
+    u.epoch = D.eb + 1;
+    u.tw = u.th = 16;
+    u.ntx = ntx16;
+    HIPC(c, launch_seed_window(u, i0, j0, i0 + w, j0 + h, st));  // no keys: u.keys null
+    unsigned long long* rst = c->d_scratch + 5;  // [visits, cells]
+    HIPC(c, hipMemsetAsync(rst, 0, 2 * sizeof(unsigned long long), st));
+    RaiseArgs ra{};
+    ra.T = dT;
+    ra.F = dF;
+    ra.ld = (int64_t)ld;
+    ra.nx = nx;
+    ra.ny = ny;
+    ra.gi = gi;
+    ra.gj = gj;
+    ra.ntx = ntx16;
+    ra.nty = nty16;
+    ra.shard_cap = D.ntiles;
+    ra.tile_epoch = c->d_tile_epoch;
+    ra.tol = 1e-13;
+    ra.stats = rst;
+    const int blocks = c->cu_count * 2;
+    uint64_t K = 4, raise_passes = 0;
+    for (;;) {
+      for (uint64_t k = 0; k < K; ++k, ++D.p) {
+        const uint64_t p = D.p;
+        if (p > D.max_passes) {
+          c->last_error = "raise: pass cap reached";
+          dom_retire(c);
+          return DYMU_ERR_NOT_CONVERGED;
+        }
+        ra.list_in = D.lists[p % 3];
+        ra.count_in = D.counts[p % 3];
+        ra.list_out = D.lists[(p + 1) % 3];
+        ra.count_out = D.counts[(p + 1) % 3];
+        ra.count_clear = D.counts[(p + 2) % 3];
+        ra.epoch = D.eb + (uint32_t)p + 2u;
+        HIPC(c, launch_raise(ra, blocks, st));
+        ++raise_passes;
+      }
+      uint64_t pending = 0;
+      rc = dom_pending(c, st, &pending);
+      if (rc) {
+        dom_retire(c);
+        return rc;
+      }
+      if (pending == 0) break;
+      K = std::min<uint64_t>(K * 2, 64);
+    }
+    unsigned long long hr[2];
+    HIPC(c, hipMemcpy(hr, rst, sizeof hr, hipMemcpyDeviceToHost));
+    c->last_update[0] = raise_passes;
+    c->last_update[1] = hr[0];
+    c->last_update[2] = hr[1];
+    // a fresh domain for the re-solve: epochs above every raise epoch (dom_retire)
+    rc = dom_begin(c, dF, dT, nx, ny, ld, 0, 0, -1, -1, st, /*cold=*/false);
+    if (rc) return rc;
+    u.shard_cap = D.ntiles;
+  }
+  u.list = D.lists[0];
+  u.counts = D.counts[0];
   u.epoch = D.eb + 1;  // the epoch of list 0 (dom_launch: eb + p + 2 for list p + 1)
   u.tw = (uint32_t)tile_w(D.variant);
   u.th = (uint32_t)tile_h(D.variant);
@@ -857,12 +935,27 @@ int resolve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_
   if (is_prio(D.variant)) {
     u.keys = prio_keys(c, 0);
     u.hist = prio_hist(c, 0);
-    HIPC(c, launch_theta_state(theta, prio_minkey(c, 0), prio_base(c, 0), st));
   }
-  if (decrease_only)
+  if (raise) {  // the cone's boundary, then the window (decreases inside it)
+    uint32_t* hist0 = u.hist;
+    u.hist = nullptr;  // binned below from the final keys (they differ per tile)
+    HIPC(c, launch_cone_seed(u, theta, st));
     HIPC(c, launch_seed_window(u, i0, j0, i0 + w, j0 + h, st));
-  else
+    if (is_prio(D.variant)) {
+      HIPC(c, launch_theta_state(theta, prio_minkey(c, 0), prio_base(c, 0), st));
+      // list 0's histogram from its keys (origin theta', the smallest boundary value):
+      // the first passes then relax the boundary tiles in key order, not all at once
+      HIPC(c, launch_rehist(D.lists[0], D.counts[0], D.ntiles, prio_keys(c, 0), prio_base(c, 0),
+                            prio_delta(c), hist0, c->d_hist + (uint64_t)4 * kShards * kBins, st));
+    }
+    return converge_auto(c, st, stats);
+  } else if (decrease_only) {
+    HIPC(c, launch_seed_window(u, i0, j0, i0 + w, j0 + h, st));
+  } else {
     HIPC(c, launch_reset_seed(u, st));
+  }
+  if (is_prio(D.variant))
+    HIPC(c, launch_theta_state(theta, prio_minkey(c, 0), prio_base(c, 0), st));
   return converge_auto(c, st, stats);
 }
 
@@ -954,6 +1047,7 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
     if (const char* kv = std::getenv("DYMU_PRIO_TRACE")) c->prio_trace = std::atoi(kv);
     if (const char* kv = std::getenv("DYMU_PRUNE")) c->prune = std::atoi(kv);
     if (const char* kv = std::getenv("DYMU_PRIO_DEBUG")) c->prio_debug = std::atoi(kv);
+    if (const char* kv = std::getenv("DYMU_RAISE")) c->raise = std::atoi(kv);
   }
   if (e == hipSuccess) e = hipMalloc(&c->d_counts, sizeof(uint32_t) * 4 * kShards);
   if (e == hipSuccess) e = hipMalloc(&c->d_scratch, sizeof(unsigned long long) * 8);
@@ -1379,6 +1473,12 @@ int dymu_pack_speed(dymu_ctx* c, uint32_t nx, uint32_t ny, uint64_t ld, double g
   a.st = cost_state(st);
   a.F = dF;
   HIPC(c, dymu::launch_pack_speed(a, pick_stream(c, stream)));
+  return DYMU_OK;
+}
+
+int dymu_last_update_stats(dymu_ctx* c, uint64_t out[4]) {
+  if (!c || !out) return DYMU_ERR_ARG;
+  std::memcpy(out, c->last_update, sizeof c->last_update);
   return DYMU_OK;
 }
 

@@ -193,6 +193,34 @@ hipError_t launch_seed_window(const UpdateArgs& a, uint32_t i0, uint32_t j0, uin
 hipError_t launch_theta_state(const unsigned long long* theta_bits, unsigned long long* minkey0,
                               double* base0, hipStream_t st);
 
+// raise front of a windowed update with speed increases (update_kernels.hip): one
+// pass over the listed 16x16 tiles; every cell whose converged value is no longer
+// supported by the update of its current neighbours under the new speed (u >
+// T (1 + tol)) becomes +inf, inside the tile until nothing changes; the tiles
+// across an edge with an invalidated cell are listed for the next pass
+struct RaiseArgs {
+  double* T;
+  const double* F;
+  int64_t ld;
+  uint32_t nx, ny, gi, gj;
+  uint32_t ntx, nty;  // 16x16 tiles
+  const uint32_t* list_in;
+  const uint32_t* count_in;
+  uint32_t* list_out;
+  uint32_t* count_out;
+  uint32_t* count_clear;
+  uint32_t shard_cap;
+  uint32_t* tile_epoch;
+  uint32_t epoch;
+  double tol;
+  unsigned long long* stats;  // [0] tile visits, [1] cells invalidated
+};
+hipError_t launch_raise(const RaiseArgs& a, int blocks, hipStream_t st);
+// after the raise: list 0 <- every tile holding a finite-speed +inf cell (not the goal)
+// next to a finite cell, key = the smallest such neighbour value of the tile (a
+// scheduling hint), histogram bin 0; *theta_bits lowered to the smallest key
+hipError_t launch_cone_seed(const UpdateArgs& a, unsigned long long* theta_bits, hipStream_t st);
+
 // early exit of computeTotalCostMap (update_kernels.hip)
 // out[0] = bits of max T over the probe cells, out[1] = *minkey (or +inf bits if null)
 hipError_t launch_probe(const double* T, int64_t ld, const ProbeCells& cells,

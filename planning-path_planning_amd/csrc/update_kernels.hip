@@ -84,10 +84,8 @@ __global__ void k_reset_seed(UpdateArgs a) {
     if (atomicMax(&a.tile_epoch[tile], a.epoch) < a.epoch) {
       const uint32_t pos = atomicAdd(&a.counts[shard], 1u);
       a.list[(uint64_t)shard * a.shard_cap + pos] = tile;
-      if (a.keys) {  // priority kernels: key theta, histogram bin 0
-        atomicMin(&a.keys[tile], *a.theta_bits);
-        atomicAdd(&a.hist[shard * kBins], 1u);
-      }
+      if (a.keys) atomicMin(&a.keys[tile], *a.theta_bits);  // priority kernels: key theta,
+      if (a.hist) atomicAdd(&a.hist[shard * kBins], 1u);    // histogram bin 0
     }
   }
 }
@@ -109,10 +107,153 @@ __global__ void k_seed_window(UpdateArgs a, uint32_t tx0, uint32_t ty0, uint32_t
     if (atomicMax(&a.tile_epoch[tile], a.epoch) < a.epoch) {
       const uint32_t pos = atomicAdd(&a.counts[shard], 1u);
       a.list[(uint64_t)shard * a.shard_cap + pos] = tile;
-      if (a.keys) {
-        atomicMin(&a.keys[tile], *a.theta_bits);
-        atomicAdd(&a.hist[shard * kBins], 1u);
+      if (a.keys) atomicMin(&a.keys[tile], *a.theta_bits);
+      if (a.hist) atomicAdd(&a.hist[shard * kBins], 1u);
+    }
+  }
+}
+
+// ---- raise front (increases inside the window) ----
+// At a converged map every free non-goal cell satisfies T = u(T) (the update of its
+// final neighbours), so after the speed of some cells went up and the cells whose
+// support is gone were set to +inf, a cell keeps its value exactly when u, computed
+// from its current neighbours under the new speed, does not exceed it.  The raise
+// repeats that test until nothing changes, starting in the window: the result is the
+// set of cells whose value depended on a raised cell (the dependency cone), every
+// other cell keeps a value some path under the new speed still realises -- a valid
+// upper bound of the new fixed point.  The FIM then re-solves the cone from its
+// boundary.  tol absorbs the last-ulp non-monotonicity of the engine's sweep sqrt
+// (<= 36 ulp): a cell kept within tol is off by at most tol relative.
+__device__ __forceinline__ double ref_update(double tx, double ty, double c) {
+  const double d = tx - ty;
+  if ((fabs(d) < c) && (tx < __builtin_inf()) && (ty < __builtin_inf()))
+    return (tx + ty + sqrt(2.0 * (c * c) - d * d)) / 2;  // :531-535
+  return fmin(tx, ty) + c;
+}
+
+constexpr int RT = 16;       // raise tile edge (kernel 5's tiling)
+constexpr int RP = RT + 2;   // image pitch
+
+__global__ __launch_bounds__(256) void k_raise(RaiseArgs a) {
+  __shared__ uint32_t s_pref[kShards + 1];
+  __shared__ double s_img[4][RP * RP];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (int k = 0; k < kShards; ++k) {
+      s_pref[k] = acc;
+      acc += a.count_in[k];
+    }
+    s_pref[kShards] = acc;
+  }
+  __syncthreads();
+  const uint32_t n = s_pref[kShards];
+  if (blockIdx.x == 0 && tid < kShards) a.count_clear[tid] = 0u;
+  const uint32_t shard = blockIdx.x % kShards;
+  double* img = s_img[wv];
+  const int r = lane >> 2, q = lane & 3;
+  const double inf = __builtin_inf();
+  unsigned long long visits = 0, cells = 0;
+  const uint32_t nw = gridDim.x * 4u;
+  for (uint32_t e = blockIdx.x * 4u + (uint32_t)wv; e < n; e += nw) {  // wave-uniform
+    int k = 0;
+    for (int s = 1; s < kShards; ++s) k += (e >= s_pref[s]) ? 1 : 0;
+    const uint32_t tile = a.list_in[(uint64_t)k * a.shard_cap + (e - s_pref[k])];
+    const int64_t i0 = (int64_t)(tile % a.ntx) * RT, j0 = (int64_t)(tile / a.ntx) * RT;
+    auto at = [&](int64_t i, int64_t j) -> double {
+      return (i >= 0 && j >= 0 && i < a.nx && j < a.ny) ? a.T[j * a.ld + i] : inf;
+    };
+    // image: own cells (r, 4q..4q+3) and the halo ring
+    double t[4], f[4];
+    bool live[4];
+    for (int c = 0; c < 4; ++c) {
+      const int64_t i = i0 + 4 * q + c, j = j0 + r;
+      const bool in = i < a.nx && j < a.ny;
+      t[c] = in ? a.T[j * a.ld + i] : inf;
+      f[c] = in ? a.F[j * a.ld + i] : inf;
+      live[c] = in && t[c] < inf && !(i == a.gi && j == a.gj);
+      img[(r + 1) * RP + 4 * q + c + 1] = t[c];
+    }
+    if (r == 0)
+      for (int c = 0; c < 4; ++c) img[4 * q + c + 1] = at(i0 + 4 * q + c, j0 - 1);
+    if (r == RT - 1)
+      for (int c = 0; c < 4; ++c) img[(RT + 1) * RP + 4 * q + c + 1] = at(i0 + 4 * q + c, j0 + RT);
+    if (q == 0) img[(r + 1) * RP] = at(i0 - 1, j0 + r);
+    if (q == 3) img[(r + 1) * RP + RT + 1] = at(i0 + RT, j0 + r);
+    __builtin_amdgcn_wave_barrier();
+    bool gone[4] = {false, false, false, false};
+    for (int it = 0; it < RT * RT; ++it) {  // a cascade is at most one cell per sweep
+      bool now[4];
+      for (int c = 0; c < 4; ++c) {
+        const int s = (r + 1) * RP + 4 * q + c + 1;
+        const double u = ref_update(fmin(img[s - 1], img[s + 1]), fmin(img[s - RP], img[s + RP]), f[c]);
+        // a cell that became an obstacle (F = +inf) loses its value outright
+        now[c] = live[c] && !gone[c] && (!(f[c] < inf) || u > t[c] * (1.0 + a.tol));
       }
+      __builtin_amdgcn_wave_barrier();
+      bool any = false;
+      for (int c = 0; c < 4; ++c)
+        if (now[c]) {
+          gone[c] = true;
+          any = true;
+          img[(r + 1) * RP + 4 * q + c + 1] = inf;
+        }
+      __builtin_amdgcn_wave_barrier();
+      if (!__any(any)) break;
+    }
+    bool edge[4] = {false, false, false, false};  // S, W, E, N
+    for (int c = 0; c < 4; ++c)
+      if (gone[c]) {
+        a.T[(j0 + r) * a.ld + i0 + 4 * q + c] = inf;
+        ++cells;
+        edge[0] |= r == 0;
+        edge[3] |= r == RT - 1;
+        edge[1] |= q == 0 && c == 0;
+        edge[2] |= q == 3 && c == 3;
+      }
+    const int tx = (int)(tile % a.ntx), ty = (int)(tile / a.ntx);
+    const int nbx[4] = {tx, tx - 1, tx + 1, tx}, nby[4] = {ty - 1, ty, ty, ty + 1};
+    for (int s = 0; s < 4; ++s) {
+      if (!__any(edge[s]) || lane != 0) continue;
+      if (nbx[s] < 0 || nby[s] < 0 || nbx[s] >= (int)a.ntx || nby[s] >= (int)a.nty) continue;
+      const uint32_t nt = (uint32_t)nby[s] * a.ntx + (uint32_t)nbx[s];
+      if (atomicMax(&a.tile_epoch[nt], a.epoch) < a.epoch) {
+        const uint32_t pos = atomicAdd(&a.count_out[shard], 1u);
+        a.list_out[(uint64_t)shard * a.shard_cap + pos] = nt;
+      }
+    }
+    ++visits;
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (lane == 0 && visits) atomicAdd(&a.stats[0], visits);
+  for (int o = 32; o > 0; o >>= 1) cells += __shfl_xor(cells, o);
+  if (lane == 0 && cells) atomicAdd(&a.stats[1], cells);
+}
+
+// List 0 after the raise (see launch_cone_seed)
+__global__ void k_cone_seed(UpdateArgs a, unsigned long long* theta_bits) {
+  const uint64_t n = (uint64_t)a.nx * a.ny;
+  const uint32_t shard = blockIdx.x % kShards;
+  const double inf = __builtin_inf();
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t j = (uint32_t)(c / a.nx), i = (uint32_t)(c % a.nx);
+    const int64_t k = (int64_t)j * a.ld + i;
+    if (!(a.T[k] == inf) || !(a.F[k] < inf) || (i == a.gi && j == a.gj)) continue;
+    double m = inf;
+    if (j > 0) m = fmin(m, a.T[k - a.ld]);
+    if (i > 0) m = fmin(m, a.T[k - 1]);
+    if (i + 1 < a.nx) m = fmin(m, a.T[k + 1]);
+    if (j + 1 < a.ny) m = fmin(m, a.T[k + a.ld]);
+    if (!(m < inf)) continue;
+    const uint32_t tile = (j / a.th) * a.ntx + (i / a.tw);
+    const unsigned long long mb = dbits(m);
+    atomicMin(theta_bits, mb);
+    if (a.keys) atomicMin(&a.keys[tile], mb);
+    if (atomicMax(&a.tile_epoch[tile], a.epoch) < a.epoch) {
+      const uint32_t pos = atomicAdd(&a.counts[shard], 1u);
+      a.list[(uint64_t)shard * a.shard_cap + pos] = tile;
+      if (a.hist) atomicAdd(&a.hist[shard * kBins], 1u);
     }
   }
 }
@@ -234,6 +375,19 @@ hipError_t launch_seed_window(const UpdateArgs& a, uint32_t i0, uint32_t j0, uin
   if (b > 1024) b = 1024;
   if (b == 0) return hipSuccess;
   hipLaunchKernelGGL(k_seed_window, dim3((unsigned)b), dim3(256), 0, st, a, tx0, ty0, tx1, ty1);
+  return hipGetLastError();
+}
+
+hipError_t launch_raise(const RaiseArgs& a, int blocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_raise, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_cone_seed(const UpdateArgs& a, unsigned long long* theta_bits, hipStream_t st) {
+  uint64_t b = ((uint64_t)a.nx * a.ny + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b == 0) b = 1;
+  hipLaunchKernelGGL(k_cone_seed, dim3((unsigned)b), dim3(256), 0, st, a, theta_bits);
   return hipGetLastError();
 }
 

@@ -113,6 +113,7 @@ FIM_SYMBOLS = {
     "dymu_memcpy_h2d": (_i32, [_vp, _vp, _vp, ctypes.c_size_t]),
     "dymu_set_profiling": (_i32, [_vp, _i32]),
     "dymu_set_pass_stats": (_i32, [_vp, _i32]),
+    "dymu_last_update_stats": (_i32, [_vp, ctypes.POINTER(_u64)]),
     "dymu_last_pass_stats": (_i32, [_vp, _vp, _u64, ctypes.POINTER(_u64)]),
     "dymu_eikonal_batch": (_i32, [_vp, _vp, _vp, _vp, _vp, _u64, _i32]),
     "dymu_slab_rows": (_i32, [_u32, _u32, _u32, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
@@ -390,6 +391,12 @@ class Engine:
 
     PASS_STAT_FIELDS = ("listed", "visited", "colour_deferred", "key_deferred", "capped",
                         "deadline", "radius_max", "sweeps", "bstar", "radius_min", "enqueued")
+
+    def last_update_stats(self) -> dict:
+        """The last windowed update's raise front (dymu_last_update_stats)."""
+        out = (_u64 * 4)()
+        _check(self._lib.dymu_last_update_stats(self.ctx, out), self.ctx)
+        return {"raise_passes": out[0], "raise_visits": out[1], "cells_invalidated": out[2]}
 
     def set_pass_stats(self, on=True):
         """Kernel 5 per-pass statistics for the next solves (diagnostics)."""

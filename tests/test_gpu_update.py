@@ -146,3 +146,38 @@ def test_resolve_window_needs_previous_solve(dymu, oracle):
         assert_parity(r.T, Tref)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("kind", ["hazard", "obstacle", "mixed", "border"])
+def test_raise_front_is_local(dymu, oracle, kind, monkeypatch):
+    """Speed increases re-propagate only the window's dependency cone (the raise
+    front), not every cell at or above theta as the round-2 reset
+    did (DYMU_RAISE=0 keeps it for A/B): both reach the cold fixed point, the raise
+    invalidates a subset of the reset region and visits fewer tiles."""
+    nx, ny, goal = 300, 260, (150, 200)
+    rng = np.random.default_rng(5)
+    F0 = oracle.synth_speed(nx, ny, seed=23, obst_frac=0.04, obst_seed=29, goal=goal)
+    F1, (i0, j0, w, h) = modified(kind, F0, goal, rng)
+    T0, _ = oracle.fmm(F0, goal)
+    Tref, _ = oracle.fmm(F1, goal)
+    got = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DYMU_RAISE", mode)
+        eng = dymu.Engine(kernel=5, prio_target=16)
+        try:
+            eng.solve(F0, *goal)
+            r = eng.resolve_window(F1, goal[0], goal[1], i0, j0, w, h)
+            got[mode] = (r, eng.last_update_stats())
+        finally:
+            eng.close()
+        assert_parity(got[mode][0].T, Tref)
+    r1, us = got["1"]
+    r0, us0 = got["0"]
+    assert us0["raise_passes"] == 0 and us["raise_passes"] > 0
+    wi0, wj0 = max(i0 - 1, 0), max(j0 - 1, 0)
+    theta = T0[wj0:j0 + h + 1, wi0:i0 + w + 1].min()
+    reset = int((np.isfinite(T0) & (T0 >= theta)).sum())
+    assert 0 < us["cells_invalidated"] <= reset
+    if kind in ("hazard", "obstacle"):  # a small cone behind a disc
+        assert us["cells_invalidated"] < 0.5 * reset
+        assert r1.stats["tile_visits"] < r0.stats["tile_visits"]

@@ -87,14 +87,31 @@ def main(N=4096, reps=5):
     eng.d2h(T0, dT0)
     for _ in range(reps):
         eng.h2d(dT, T0)
+        eng.d2h(np.empty(1), dT)  # drain
+        t = time.perf_counter()
         sw = eng.resolve_window_device(dF, dT, N, N, N, goal[0], goal[1], i0, j0, w, w)
-        tw.append(sw["ms"])
+        tw.append((time.perf_counter() - t) * 1e3)  # raise front + re-solve, wall
+    us = eng.last_update_stats()
     Tw = np.empty((N, N))
     eng.d2h(Tw, dT)
+    # A/B: the round-2 theta reset (every cell at or above theta) on the same bump
+    os.environ["DYMU_RAISE"] = "0"
+    eng_r = dymu.Engine()
+    del os.environ["DYMU_RAISE"]
+    tr, sr = [], None
+    for _ in range(reps):
+        eng_r.h2d(dT, T0)
+        eng_r.d2h(np.empty(1), dT)
+        t = time.perf_counter()
+        sr = eng_r.resolve_window_device(dF, dT, N, N, N, goal[0], goal[1], i0, j0, w, w)
+        tr.append((time.perf_counter() - t) * 1e3)
+    eng_r.close()
     tcold, sc = [], None
     for _ in range(reps):
+        eng.d2h(np.empty(1), dT)
+        t = time.perf_counter()
         sc = eng.solve_device(dF, dT, N, N, N, *goal)
-        tcold.append(sc["ms"])
+        tcold.append((time.perf_counter() - t) * 1e3)
     Tc = np.empty((N, N))
     eng.d2h(Tc, dT)
     # the disc cleared again: a decrease-only change (no reset, window tiles seeded)
@@ -113,13 +130,18 @@ def main(N=4096, reps=5):
     td, sd = [], None
     for _ in range(reps):
         eng.h2d(dT, Tb)
+        eng.d2h(np.empty(1), dT)
+        t = time.perf_counter()
         sd = eng.update_window_device(dF, dT, N, N, N, goal[0], goal[1], i0, j0, w, w, True)
-        td.append(sd["ms"])
+        td.append((time.perf_counter() - t) * 1e3)
     Td = np.empty((N, N))
     eng.d2h(Td, dT)
     tcold2 = []
     for _ in range(reps):
-        tcold2.append(eng.solve_device(dF, dT, N, N, N, *goal)["ms"])
+        eng.d2h(np.empty(1), dT)
+        t = time.perf_counter()
+        eng.solve_device(dF, dT, N, N, N, *goal)
+        tcold2.append((time.perf_counter() - t) * 1e3)
     fin0 = np.isfinite(T0c)
     out["config5_clear"] = {
         "decrease_only_ms": float(np.median(td)), "cold_ms": float(np.median(tcold2)),
@@ -134,6 +156,10 @@ def main(N=4096, reps=5):
         "window": [i0, j0, w, w], "windowed_ms": float(np.median(tw)),
         "cold_ms": float(np.median(tcold)), "speedup": float(np.median(tcold) / np.median(tw)),
         "windowed_tile_visits": sw["tile_visits"], "cold_tile_visits": sc["tile_visits"],
+        "windowed_passes": sw["passes"], "raise": us,
+        "theta_reset_ms": float(np.median(tr)), "theta_reset_tile_visits": sr["tile_visits"],
+        "theta_reset_passes": sr["passes"],
+        "timing": "wall clock around the blocking C-ABI call (raise front included)",
         "inf_mask_equal": bool(np.array_equal(np.isinf(Tw), np.isinf(Tc))),
         "max_rel_diff_vs_cold": float((np.abs(Tw[fin] - Tc[fin]) / np.maximum(1, Tc[fin])).max()),
         "bitwise_equal_frac": float((Tw == Tc).mean()),

@@ -8,14 +8,15 @@ TAG=${TAG:-r03}
 O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/gputest.log 2>&1
+timeout -k 10 900 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/gputest.log 2>&1
 rc=$?
 grep -E "passed|failed|error" $O/gputest.log | tail -3
 if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" $O/gputest.log | head -30; tail -40 $O/gputest.log; exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo smoke failed; cat $O/smoke.log; exit 1; }
 cat $O/smoke.log
-timeout -k 10 200 python tools/pass_decomp.py --out $O --tag decomp16k > $O/decomp16k.json 2> $O/decomp16k.err || { echo decomp failed; tail -20 $O/decomp16k.err; exit 1; }
-cat $O/decomp16k.json
+[ -n "$NO_DECOMP" ] || timeout -k 10 200 python tools/pass_decomp.py --out $O --tag decomp16k > $O/decomp16k.json 2> $O/decomp16k.err || { echo decomp failed; tail -20 $O/decomp16k.err; exit 1; }
+[ -n "$NO_DECOMP" ] || cat $O/decomp16k.json
+[ -n "$CONFIGS" ] && { timeout -k 10 300 python tools/configs.py > $O/configs_4096.json 2> $O/configs.err || { echo configs failed; tail $O/configs.err; exit 1; }; cat $O/configs_4096.json; }
 [ -n "$NO_BENCH" ] && exit 0
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || { echo bench failed; tail -20 $O/bench.err; exit 1; }
 timeout -k 10 300 python bench.py --sharded --steps 5 --cpu-sample 0 > $O/bench_sharded_n1.json 2> $O/bench_sharded_n1.err || { echo sharded n1 failed; tail -20 $O/bench_sharded_n1.err; exit 1; }
