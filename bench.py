@@ -160,7 +160,7 @@ PROFILE_PERIOD = 64  # time every 64th pass launch with HIP events (sampled mean
 # 8th added 3% to the solve, every 32nd 1.3%)
 _EXACT = os.environ.get("DYMU_EXACT_SQRT", "0") not in ("", "0")  # dymu_opts.exact_sqrt
 KERNEL_NAMES = {3: "k_fim_pass_rb", 4: "k_fim_pass_prio<8>",
-                5: f"k_fim_pass_dyn<16, {'false' if _EXACT else 'true'}>"}
+                5: f"k_fim_pass_dyn<16, {'false' if _EXACT else 'true'}, false>"}
 
 
 def geometric_bound(N, gi, gj, tw, th):

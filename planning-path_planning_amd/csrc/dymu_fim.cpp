@@ -117,6 +117,11 @@ struct dymu_ctx {
   // kShards x kPsWords words, pass p at p % kPassStatCap
   int pass_stats = 0;
   uint32_t* d_pstat = nullptr;
+  // kernel 5 edge columns (PassArgs::ec): 32 doubles per 16x16 tile; 1.5-2% per
+  // 16384^2 solve against the per-row W / E halo loads (profiles/r03/ec)
+  int use_ec = 1;
+  double* d_ec = nullptr;
+  uint64_t ec_cap = 0;  // tiles
   // windowed updates with increases: theta reset (0, default) or the raise front (1,
   // DYMU_RAISE=1: exact dependency cone, measured slower on config 5 -- 9.5 vs 4.1 ms
   // at 4096^2, profiles/r03/configs_4096_r03c.json); the last
@@ -308,6 +313,26 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
     if (is_prio(D.variant))
       HIPC(c, launch_prio_seed(c->d_keys, c->d_hist, c->d_prio, gtile, 0.0, st));
   }
+  // kernel 5 edge columns: +inf (cold) plus the goal's tile; a warm domain
+  // (resolve_core) rebuilds them from T once its seeding kernels have run (ec_sync)
+  a.ec = nullptr;
+  if (D.variant == 5 && c->use_ec) {
+    if (c->ec_cap < ntiles) {
+      if (c->d_ec) (void)hipFree(c->d_ec);
+      c->d_ec = nullptr;
+      c->ec_cap = 0;
+      HIPC(c, hipMalloc(&c->d_ec, sizeof(double) * 32 * (uint64_t)ntiles));
+      c->ec_cap = ntiles;
+    }
+    a.ec = c->d_ec;
+    if (cold) {
+      HIPC(c, launch_fill_inf(c->d_ec, 0, 32u * ntiles, 0, 1, st));
+      if (gj >= 0) {
+        const uint32_t gtile = (uint32_t)(gj / THd) * ntx + (uint32_t)(gi / TWd);
+        HIPC(c, launch_ec_rebuild(dT, ld, nx, nrows, c->d_ec, ntx, gtile, gtile + 1, st));
+      }
+    }
+  }
   a.F = dF;
   a.T = dT;
   a.ld = (int64_t)ld;
@@ -327,6 +352,7 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
                 : variant == 5            ? 16
                                           : 4 * (TWd + THd);
   if (const char* kv = std::getenv("DYMU_MAX_INNER")) a.max_inner = std::max(1, std::atoi(kv));
+
   a.sweep_deadline = (variant == 5 && big) ? 1400u : 0u;  // 10-ns s_memrealtime ticks
   if (const char* kv = std::getenv("DYMU_SWEEP_DEADLINE"))
     a.sweep_deadline = (uint32_t)std::max(0, std::atoi(kv));
@@ -948,6 +974,8 @@ int resolve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_
       HIPC(c, launch_rehist(D.lists[0], D.counts[0], D.ntiles, prio_keys(c, 0), prio_base(c, 0),
                             prio_delta(c), hist0, c->d_hist + (uint64_t)4 * kShards * kBins, st));
     }
+    if (D.a.ec)
+      HIPC(c, launch_ec_rebuild(dT, ld, nx, ny, D.a.ec, (uint32_t)D.a.ntx, 0, D.ntiles, st));
     return converge_auto(c, st, stats);
   } else if (decrease_only) {
     HIPC(c, launch_seed_window(u, i0, j0, i0 + w, j0 + h, st));
@@ -956,6 +984,8 @@ int resolve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_
   }
   if (is_prio(D.variant))
     HIPC(c, launch_theta_state(theta, prio_minkey(c, 0), prio_base(c, 0), st));
+  if (D.a.ec)  // the reset kernel wrote T
+    HIPC(c, launch_ec_rebuild(dT, ld, nx, ny, D.a.ec, (uint32_t)D.a.ntx, 0, D.ntiles, st));
   return converge_auto(c, st, stats);
 }
 
@@ -1090,6 +1120,7 @@ int dymu_destroy(dymu_ctx* c) {
   if (c->d_prio) (void)hipFree(c->d_prio);
   if (c->d_trace) (void)hipFree(c->d_trace);
   if (c->d_pstat) (void)hipFree(c->d_pstat);
+  if (c->d_ec) (void)hipFree(c->d_ec);
   if (c->d_lut) (void)hipFree(c->d_lut);
   if (c->d_scratch) (void)hipFree(c->d_scratch);
   if (c->d_xchg) (void)hipFree(c->d_xchg);

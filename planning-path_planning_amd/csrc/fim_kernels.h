@@ -81,6 +81,12 @@ struct PassArgs {
   uint32_t* tot_save;       // block 0 stores the pass's count here ...
   const uint32_t* tot_prev;  // ... and a later pass stores *tot_prev + its count
   int32_t* tot_out;          //     into *tot_out (the round's termination count)
+  // ---- kernel 5: edge columns (required) ----
+  // ec[t * 32 + 0..15] = column 0 (W edge) of tile t's T, ec[t * 32 + 16..31] = column
+  // 15 (E edge): an interior tile reads its W / E halo as ONE 128-byte line of its
+  // neighbour's edge instead of one line per row; every visit writes its decreased
+  // edge cells here too ("Edge columns")
+  double* ec;
   // ---- kernel 5, per-pass statistics (dymu_set_pass_stats; off = null) ----
   // this pass's record: kShards rows of kPsWords words (PassStat), one row per
   // workgroup shard, summed (max / min for the radii) by the host
@@ -136,6 +142,9 @@ hipError_t launch_exchange(double* T, int64_t ld, int64_t nx, int64_t nrows, con
 hipError_t launch_eikonal_batch(const double* tx, const double* ty, const double* c, double* out,
                                 uint64_t n, int fast, hipStream_t st);
 hipError_t launch_sum_counts(const uint32_t* counts, int32_t* out, hipStream_t st);
+// edge columns of tiles [t0, t1) (16x16 tiles, ntx per row) from T (see PassArgs::ec)
+hipError_t launch_ec_rebuild(const double* T, uint64_t ld, uint32_t nx, uint32_t ny, double* ec,
+                             uint32_t ntx, uint32_t t0, uint32_t t1, hipStream_t st);
 // deterministic mode: rebuild the key histogram of a list from its FINAL keys (the
 // enqueue path bins a tile by the key of its first insertion, which depends on the
 // order of the insertions) into shard 0's row of `out`; `zero` (the other of two

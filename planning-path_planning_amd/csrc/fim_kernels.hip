@@ -733,6 +733,7 @@ template <bool APPROX = false, class Gate = NoGate>
 __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned long long* ek,
                                        bool has, int tx, int ty, int lane, bool& capped,
                                        Gate gate = Gate(), unsigned long long stop_at = ~0ull) {
+  const int cap = a.max_inner;
   constexpr int TT = 16;
   const int r = lane >> 2, q = lane & 3, odd = r & 1;
   const int cr[2] = {4 * q + odd, 4 * q + 2 + odd};
@@ -762,8 +763,11 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
       tb[k] = Tr[cb[k]];
       fb[k] = Fr[cb[k]];
     }
-    hw = Tr[-1];
-    he = Tr[TT];
+    {  // the neighbours' edge columns: one line each instead of 16
+      const double* e = a.ec + ((uint64_t)ty * (uint64_t)a.ntx + (uint64_t)tx) * 32 + r;
+      hw = e[-32 + 16];
+      he = e[32];
+    }
     const double* Ts = a.T + (j0 - 1) * a.ld + i0 + 4 * q;
     const double* Tn = a.T + (j0 + TT) * a.ld + i0 + 4 * q;
 #pragma unroll
@@ -826,10 +830,10 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
   const bool fast = __all(!(fr[0] < kFastMinF) && !(fr[1] < kFastMinF) &&
                           !(fb[0] < kFastMinF) && !(fb[1] < kFastMinF));
   const int sweeps =
-      fast ? rb_sweeps4<true, APPROX>(img + sr[0], img + sb[0], dn, ds, fr, fb, tr, tb,
-                                      a.max_inner, capped, stop_at)
-           : rb_sweeps4<false>(img + sr[0], img + sb[0], dn, ds, fr, fb, tr, tb, a.max_inner,
-                               capped, stop_at);
+      fast ? rb_sweeps4<true, APPROX>(img + sr[0], img + sb[0], dn, ds, fr, fb, tr, tb, cap,
+                                      capped, stop_at)
+           : rb_sweeps4<false>(img + sr[0], img + sb[0], dn, ds, fr, fb, tr, tb, cap, capped,
+                               stop_at);
   // write back decreased cells; dr/db: the decreased value or +inf.  Keys are
   // non-negative doubles, so the u64 order of their bits (ek) is their f64
   // order and the edge minima below are v_min_f64 / v_cmp_f64 work.
@@ -857,6 +861,7 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
   }
   if (q == 0 || q == 3) {  // W / E edge: column 0 (cr[0] or cb[0]) / column 15 (cr[1] or cb[1])
     const double c = q == 0 ? (odd ? db[0] : dr[0]) : (odd ? dr[1] : db[1]);
+    if (c < dinf()) a.ec[((uint64_t)ty * (uint64_t)a.ntx + (uint64_t)tx) * 32 + (q == 0 ? 0 : 16) + r] = c;
     const double m = across(c, img[q == 0 ? rb - 1 : rb + TT]);
     if (m < dinf()) atomicMin(&ek[q == 0 ? 1 : 2], dbits(m));
   }
@@ -1078,7 +1083,10 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_prio(PassArgs a) {
 // bin) or visits it.  No classify phase and no block-wide barrier between
 // reading the list and the sweeps: a wave that drew a deferred or a quickly
 // converging tile moves on to the next entry while the others still sweep.
-template <int WPB, bool APPROX>
+// STATS: the per-pass statistics (a.pstat) are counted -- a separate instantiation,
+// so the default kernel carries none of it (it cost 2% per solve inline: SGPR
+// spills 31 -> 41, profiles/r03/knobs1)
+template <int WPB, bool APPROX, bool STATS = false>
 __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   constexpr int IMG = IMG16;
   __shared__ uint32_t s_q[QCAP];
@@ -1152,7 +1160,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
         atomicAdd(&a.stats[kStatPasses], 1ull);
         atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
       }
-      if (a.pstat) {
+      if (STATS && a.pstat) {
         a.pstat[kPsActive] = n_active;
         a.pstat[kPsBstar] = (uint32_t)bstar;
       }
@@ -1203,7 +1211,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
         enqueue(tile, k0);
       }
       ++my_defer;
-      if (a.pstat) ++my_cd;
+      if (STATS && a.pstat) ++my_cd;
       continue;
     }
     const unsigned long long kb = a.key_in[tile];
@@ -1227,7 +1235,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     my_visits += 1;
     my_sweeps += (unsigned long long)sweeps;
     const bool cap = __any(capped);
-    if (a.pstat) {
+    if (STATS && a.pstat) {
       if (cap) {
         if (sweeps >= a.max_inner) ++my_cap;
         else ++my_dl;
@@ -1297,7 +1305,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     atomicAdd(&s_visits, my_visits);
     atomicAdd(&s_sweeps, my_sweeps);
     atomicAdd(&s_defer, my_defer);
-    if (a.pstat) {
+    if (STATS && a.pstat) {
       atomicAdd(&s_ps[0], my_cd);
       atomicAdd(&s_ps[1], my_cap);
       atomicAdd(&s_ps[2], my_dl);
@@ -1316,7 +1324,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       atomicAdd(&st[kStatSweeps], s_sweeps);
       if (s_defer) atomicAdd(&st[kStatDeferred], s_defer);
     }
-    if (a.pstat) {  // one row per shard: 16 workgroups per address
+    if (STATS && a.pstat) {  // one row per shard: 16 workgroups per address
       uint32_t* ps = a.pstat + (uint64_t)shard * kPsWords;
       atomicAdd(&ps[kPsVisited], (uint32_t)s_visits);
       atomicAdd(&ps[kPsColour], s_ps[0]);
@@ -1504,6 +1512,19 @@ __global__ void k_exchange(MergeArgs g, const double* new_lo, const double* new_
   }
 }
 
+// edge columns (PassArgs::ec) of tiles [t0, t1) from T: one thread per (tile, side, row)
+__global__ void k_ec_rebuild(const double* T, uint64_t ld, uint32_t nx, uint32_t ny, double* ec,
+                             uint32_t ntx, uint32_t t0, uint32_t t1) {
+  const uint64_t n = (uint64_t)(t1 - t0) * 32;
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t t = t0 + c / 32;
+    const uint32_t k = (uint32_t)(c % 32), side = k / 16, r = k % 16;
+    const uint64_t j = (t / ntx) * 16 + r, i = (t % ntx) * 16 + (side ? 15 : 0);
+    ec[t * 32 + k] = (i < nx && j < ny) ? T[j * ld + i] : dinf();
+  }
+}
+
 __global__ void k_sum_counts(const uint32_t* counts, int32_t* out) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     uint32_t s = 0;
@@ -1577,19 +1598,22 @@ hipError_t launch_pass_prio(const PassArgs& a, int blocks, hipStream_t st, hipEv
   return hipGetLastError();
 }
 
-template <int WPB, bool APPROX>
+template <int WPB, bool APPROX, bool STATS = false>
 hipError_t launch_dyn_k(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
                         hipEvent_t e1) {
   if (e0 || e1)
-    hipExtLaunchKernelGGL((k_fim_pass_dyn<WPB, APPROX>), dim3(blocks), dim3(64 * WPB), 0, st, e0,
+    hipExtLaunchKernelGGL((k_fim_pass_dyn<WPB, APPROX, STATS>), dim3(blocks), dim3(64 * WPB), 0, st, e0,
                           e1, 0, a);
   else
-    hipLaunchKernelGGL((k_fim_pass_dyn<WPB, APPROX>), dim3(blocks), dim3(64 * WPB), 0, st, a);
+    hipLaunchKernelGGL((k_fim_pass_dyn<WPB, APPROX, STATS>), dim3(blocks), dim3(64 * WPB), 0, st, a);
   return hipGetLastError();
 }
 // kernel 5: 16-wave workgroups, the sweep sqrt of a.exact_sqrt
 hipError_t launch_pass_prio16(const PassArgs& a, int blocks, hipStream_t st, hipEvent_t e0,
                               hipEvent_t e1) {
+  if (a.pstat)
+    return a.exact_sqrt ? launch_dyn_k<16, false, true>(a, blocks, st, e0, e1)
+                        : launch_dyn_k<16, true, true>(a, blocks, st, e0, e1);
   return a.exact_sqrt ? launch_dyn_k<16, false>(a, blocks, st, e0, e1)
                       : launch_dyn_k<16, true>(a, blocks, st, e0, e1);
 }
@@ -1711,6 +1735,17 @@ hipError_t launch_rehist(const uint32_t* list, const uint32_t* counts, uint32_t 
                          uint32_t* out, uint32_t* zero, hipStream_t st) {
   hipLaunchKernelGGL(k_rehist, dim3(8, kShards), dim3(256), 0, st, list, counts, cap, keys, base,
                      delta, out, zero);
+  return hipGetLastError();
+}
+
+hipError_t launch_ec_rebuild(const double* T, uint64_t ld, uint32_t nx, uint32_t ny, double* ec,
+                             uint32_t ntx, uint32_t t0, uint32_t t1, hipStream_t st) {
+  const uint64_t n = (uint64_t)(t1 - t0) * 32;
+  uint64_t b = (n + 255) / 256;
+  if (b > 16384) b = 16384;
+  if (b == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ec_rebuild, dim3((unsigned)b), dim3(256), 0, st, T, ld, nx, ny, ec, ntx, t0,
+                     t1);
   return hipGetLastError();
 }
 
