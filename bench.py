@@ -66,6 +66,8 @@ def parse():
                          "python loop; tools/vdist_rehearsal.py)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the row-slab path even at N=1 (exercises the RCCL code path)")
+    ap.add_argument("--cpu-linear-size", type=int, default=1024,
+                    help="edge of the grid the reference's linear-scan band is timed on")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the exact-sqrt / deterministic re-runs of the headline solve")
     ap.add_argument("--no-planner", action="store_true",
@@ -152,6 +154,30 @@ def cpu_reference_algorithm(n_edge, obst):
         "sample": f"{n_edge}x{n_edge} config-3 grid, oracle FMM with the reference's linear-scan "
                   f"narrow band (:551-568), 1 thread, {dt:.1f}s; the rate falls with grid size "
                   f"(O(cells x band))",
+    }
+
+
+def cpu_parallel(n_edge, obst):
+    """SURVEY s8(d) cpu_fim_omp (optional): the same fixed point on ALL the host threads the
+    job may use (OMP_NUM_THREADS, else every CPU) -- oracle_par.c's block FIM with a
+    warm-started fast-marching solve per 64x64 tile."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi
+
+    o = oracle_ffi.load()
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
+    g = (n_edge // 2, n_edge // 2)
+    F = o.synth_speed(n_edge, n_edge, seed=1, obst_frac=obst, obst_seed=3, goal=g)
+    t0 = time.perf_counter()
+    _, passes = o.fim_parallel(F, g, threads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": n_edge * n_edge / dt / 1e6,
+        "unit": "Mcells/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n_edge}x{n_edge} config-3 grid, block FIM (64x64 tiles, local fast marching) "
+                  f"on {threads} threads, {passes} passes, {dt:.1f}s; same fixed point as the FMM",
     }
 
 
@@ -428,7 +454,8 @@ def main():
         }
     if world == 1 and args.cpu_sample > 0 and not args.fake_cpu:
         line["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.obst)
-        line["cpu_reference_algorithm"] = cpu_reference_algorithm(1024, args.obst)
+        line["cpu_reference_algorithm"] = cpu_reference_algorithm(args.cpu_linear_size, args.obst)
+        line["cpu_parallel"] = cpu_parallel(args.cpu_sample, args.obst)
     print(json.dumps(line), flush=True)
     if line.get("parity") is not None and not line["parity"]["ok"]:
         sys.exit(f"bench: the stitched map failed its self-check: {line['parity']}")

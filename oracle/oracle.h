@@ -86,6 +86,13 @@ int oracle_fmm_heap(const double* F, uint32_t nx, uint32_t ny, uint32_t gi, uint
                     int64_t start_i, int64_t start_j, double* T, uint8_t* closed,
                     uint64_t* n_pops);
 
+/* All-cores CPU baseline (oracle_par.c, SURVEY s8(d) cpu_fim_omp): the same fixed
+ * point reached by a block FIM over `threads` OpenMP threads (64 x 64 tiles, a
+ * warm-started fast-marching solve inside a tile).  Equals oracle_fmm_heap within ulps.
+ * Returns 0, or -1 on bad arguments; *passes = parallel passes. */
+int oracle_fim_parallel(const double* F, uint32_t nx, uint32_t ny, uint32_t gi, uint32_t gj,
+                        double* T, int threads, uint64_t* passes);
+
 /* Jacobi iteration of the same update to its fixed point from T=+inf
  * (SURVEY s8(c)); returns the number of sweeps.  Used by property tests. */
 int oracle_jacobi(const double* F, uint32_t nx, uint32_t ny, uint32_t gi, uint32_t gj, double* T,

@@ -35,6 +35,8 @@ _SIGS = {
     "oracle_fmm_heap": (ctypes.c_int, [_dp, _u32, _u32, _u32, _u32, _i64, _i64, _dp, _vp,
                                        ctypes.POINTER(_u64)]),
     "oracle_jacobi": (ctypes.c_int, [_dp, _u32, _u32, _u32, _u32, _dp, ctypes.c_int]),
+    "oracle_fim_parallel": (ctypes.c_int, [_dp, _u32, _u32, _u32, _u32, _dp, ctypes.c_int,
+                                           ctypes.POINTER(_u64)]),
     "oracle_residual": (_d, [_dp, _dp, _u32, _u32, _u32, _u32, ctypes.POINTER(_u64)]),
     "oracle_total_cost_matrix": (None, [_dp, _u64, _dp]),
     "oracle_global_path": (ctypes.c_int, [_dp, _vp, _u32, _u32, _d, _u32, _u32, _d, _d, _d, _d,
@@ -187,6 +189,17 @@ class Oracle:
             F = F.reshape(ny, nx)
             F[o] = np.inf
         return F.reshape(ny, nx)
+
+    def fim_parallel(self, F, goal, threads=4):
+        """All-cores block FIM (oracle_par.c): (T, passes)."""
+        F = np.ascontiguousarray(F, dtype=np.float64)
+        ny, nx = F.shape
+        T = np.empty_like(F)
+        passes = _u64()
+        rc = self.lib.oracle_fim_parallel(F, nx, ny, goal[0], goal[1], T, threads,
+                                          ctypes.byref(passes))
+        assert rc == 0
+        return T, passes.value
 
     def fmm(self, F, goal, start=None, linear=False, want_closed=False):
         F = np.ascontiguousarray(F, dtype=np.float64)

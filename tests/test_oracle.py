@@ -179,3 +179,17 @@ def test_path_extraction_straight_line(oracle):
     assert wp[-1, 0] == 40.0 and wp[-1, 1] == 32.0
     steps = np.diff(wp[:-1, 0])
     assert np.allclose(steps, 0.4)
+
+
+@pytest.mark.parametrize("N,frac,threads", [(300, 0.04, 4), (517, 0.0, 8), (1024, 0.02, 8)])
+def test_parallel_cpu_fim_matches_fmm(oracle, N, frac, threads):
+    """The all-cores CPU baseline (oracle_par.c) reaches the FMM's fixed point:
+    identical +inf mask, every finite cell within 1e-12."""
+    g = (N // 3, N // 2)
+    F = oracle.synth_speed(N, N, seed=9, obst_frac=frac, obst_seed=10, goal=g)
+    Tp, passes = oracle.fim_parallel(F, g, threads=threads)
+    Tr, _ = oracle.fmm(F, g)
+    assert np.array_equal(np.isinf(Tp), np.isinf(Tr))
+    fin = np.isfinite(Tr)
+    assert (np.abs(Tp[fin] - Tr[fin]) / np.maximum(1, Tr[fin])).max() <= 1e-12
+    assert passes >= 1
