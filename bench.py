@@ -66,7 +66,7 @@ def parse():
                          "python loop; tools/vdist_rehearsal.py)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the row-slab path even at N=1 (exercises the RCCL code path)")
-    ap.add_argument("--cpu-linear-size", type=int, default=1024,
+    ap.add_argument("--cpu-linear-size", type=int, default=2048,
                     help="edge of the grid the reference's linear-scan band is timed on")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the exact-sqrt / deterministic re-runs of the headline solve")

@@ -12,6 +12,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -67,3 +68,24 @@ def test_bench_world_mismatch_fails():
                          capture_output=True, text=True, timeout=120)
     assert out.returncode != 0
     assert "WORLD_SIZE=3" in out.stderr
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_ipc_one_gpu_self_check():
+    """The multi-GPU bench path end to end on the one GPU of a test box: `bench.py
+    --gpus 2 --exchange ipc` spawns two ranks (torch.distributed.run), both on
+    device 0, runs the native round loop over the IPC transport, and its
+    self-check (slab residual, ghost rows, sum / count vs a single-GPU solve) must
+    pass -- the code the driver's N-GPU run executes, with RCCL's P2P swapped for
+    IPC because RCCL refuses two ranks on one GPU."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--exchange", "ipc", "--size", "2048", "--steps", "2", "--warmup", "1",
+                          "--cpu-sample", "0"],
+                         env=_env(DYMU_DIST_TIMEOUT_S="60"), cwd=ROOT, capture_output=True,
+                         text=True, timeout=280)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["n_gpus"] == 2 and rec["config"]["ranks_seen"] == 2
+    par = rec["parity"]
+    assert par["ok"] and par["ghost_max_abs_diff"] == 0 and par["mismatched_cells"] == 0
+    assert par["finite_cells"] == par["finite_cells_single"] > 0.9 * 2048 * 2048

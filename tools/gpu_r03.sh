@@ -21,5 +21,6 @@ cat $O/smoke.log
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || { echo bench failed; tail -20 $O/bench.err; exit 1; }
 timeout -k 10 300 python bench.py --sharded --steps 5 --cpu-sample 0 > $O/bench_sharded_n1.json 2> $O/bench_sharded_n1.err || { echo sharded n1 failed; tail -20 $O/bench_sharded_n1.err; exit 1; }
 timeout -k 10 400 python bench.py --gpus 2 --exchange ipc --steps 3 --warmup 1 --cpu-sample 0 > $O/bench_ipc_n2.json 2> $O/bench_ipc_n2.err || { echo ipc n2 failed; tail -20 $O/bench_ipc_n2.err; exit 1; }
+[ -n "$LINEAR2048" ] && { timeout -k 10 600 python bench.py --steps 2 --warmup 1 --no-planner --no-variants --cpu-linear-size 2048 > $O/bench_linear2048.json 2> $O/bench_linear2048.err || { echo linear2048 failed; tail $O/bench_linear2048.err; exit 1; }; }
 for f in bench bench_sharded_n1 bench_ipc_n2; do python -c "
 import json; d=json.loads(open('$O/$f.json').read().strip().splitlines()[-1]); print('$f', d['value'], d['ms_per_step'], d.get('parity'), d.get('variants'))"; done
