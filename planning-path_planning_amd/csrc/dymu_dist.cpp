@@ -486,9 +486,12 @@ class IpcTransport final : public Transport {
     board[rank].pre.store((s << 1) | (ok ? 1u : 0u), std::memory_order_release);
     bool all = true;
     for (int q = 0; q < world; ++q) {
-      if (!spin_until([&] { return (board[q].pre.load(std::memory_order_acquire) >> 1) >= s; }))
-        return fail(err, "dymu_dist_solve", "timed out in the pre-flight (a peer rank failed?)",
-                    DYMU_ERR_RCCL);
+      if (!spin_until([&] { return (board[q].pre.load(std::memory_order_acquire) >> 1) >= s; })) {
+        const std::string why = "timed out in the pre-flight of solve " + std::to_string(s) +
+                                " waiting for rank " + std::to_string(q) + " (at solve " +
+                                std::to_string(board[q].pre.load() >> 1) + "; a peer rank failed?)";
+        return fail(err, "dymu_dist_solve", why.c_str(), DYMU_ERR_RCCL);
+      }
       all = all && (board[q].pre.load(std::memory_order_acquire) & 1u);
     }
     if (!all)

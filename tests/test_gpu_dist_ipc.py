@@ -15,8 +15,11 @@ pytestmark = pytest.mark.gpu
 
 
 def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank):
-    os.environ.setdefault("DYMU_DIST_TIMEOUT_S", "60")
+    os.environ.setdefault("DYMU_DIST_TIMEOUT_S", "90")
     import sys
+    import time
+    t0 = time.monotonic()
+    marks = []
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "planning-path_planning_amd"))
     import dymu
@@ -26,6 +29,7 @@ def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank):
         row0, nrows = dymu.slab_rows(ny, world, rank)
         eng = dymu.Engine(device=0, **engine_kw)
         solver = dist.DistSolver(eng, 0, uid, rank, world, transport="ipc")
+        marks.append(("joined", round(time.monotonic() - t0, 2)))
         seen = solver.comm_count()
         dF = eng.alloc(8 * nrows * nx)
         dT = eng.alloc(8 * (nrows + 2) * nx)
@@ -37,6 +41,7 @@ def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank):
                 pre = "solved"
             except dymu.DymuError as e:
                 pre = e.status
+            marks.append(("preflight", round(time.monotonic() - t0, 2)))
         sts = [solver.solve(dF, dT, nx, nx, ny, goal[0], goal[1], 4) for _ in range(2)]
         T = np.empty((nrows, nx))
         eng.d2h(T, dT + 8 * nx)
@@ -46,7 +51,8 @@ def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank):
         eng.close()
         out_q.put((rank, row0, T, [s["rounds"] for s in sts], seen, pre, None))
     except Exception as e:  # reported to the parent, which fails the test
-        out_q.put((rank, 0, None, None, 0, None, repr(e)))
+        marks.append(("error", round(time.monotonic() - t0, 2)))
+        out_q.put((rank, 0, None, None, 0, None, f"rank {rank}: {e!r} {marks}"))
 
 
 def _run(oracle, world, nx, ny, goal, engine_kw, bad_rank=None):
