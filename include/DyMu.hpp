@@ -149,7 +149,8 @@ class DyMuPathPlanner {
   int repairPath(base::Waypoint wInit, unsigned index);
   bool evaluatePath(unsigned starting_index);
   void expandRisk();
-  // the set node, or std::nullopt (the reference's NULL)
+  // the set node, or std::nullopt (the reference's NULL; also after the
+  // wall-clock limit, 5 s as in src/DyMu_LocalPathRepairing.cpp:685-696)
   std::optional<localNode> computeLocalPropagation(base::Waypoint wInit, base::Waypoint wOvertake);
   std::vector<base::Waypoint> getLocalPath(const localNode& lSetNode, base::Waypoint wInit,
                                            double tau);
@@ -163,6 +164,10 @@ class DyMuPathPlanner {
   int getReconnectingIndex();
 
   // -- extensions (not in the reference) --
+  // computeLocalPropagation's wall-clock limit in seconds (the reference's fixed
+  // 5.0, :685-696); <= 0 disables it
+  void setLocalPropagationTimeout(double seconds) { local_timeout_s_ = seconds; }
+  double localPropagationTimeout() const { return local_timeout_s_; }
   // Flat row-major views for FFI callers (ny*nx, index j*nx + i).  The total
   // cost lives on the device; this downloads whatever the host copy lacks.
   const double* totalCostData() const;
@@ -250,6 +255,7 @@ class DyMuPathPlanner {
   repairingAproach repairing_approach_;
   unsigned nx_ = 0, ny_ = 0;
   double global_res_ = 1.0, local_res_ = 1.0;
+  double local_timeout_s_ = 5.0;
   unsigned res_ratio_ = 1;
   std::unique_ptr<LocalLayer> local_;
   std::vector<double> global_offset_{0.0, 0.0};

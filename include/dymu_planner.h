@@ -120,6 +120,9 @@ int dymu_planner_expand_risk(dymu_planner* p);
 /* computeLocalPropagation (:578-698): 1 and the set node's global pose, or 0 (NULL) */
 int dymu_planner_compute_local_propagation(dymu_planner* p, const double* start_xyzh,
                                            const double* overtake_xyzh, double* set_xy);
+/* computeLocalPropagation's wall-clock limit (the reference's 5 s, :685-696;
+ * <= 0 disables it); it then returns 0 (NULL) like the reference */
+int dymu_planner_set_local_timeout(dymu_planner* p, double seconds);
 /* getRiskMatrix / getDeviationMatrix (:1111-1211): (21*r)^2 doubles, r = res ratio */
 int dymu_planner_get_risk_matrix(dymu_planner* p, double x, double y, double z, double heading,
                                  double* out);

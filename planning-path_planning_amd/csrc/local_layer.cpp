@@ -12,6 +12,8 @@
 // Where the reference has undefined behaviour the definitions U1-U5 of
 // DESIGN.md s4.7 apply (the oracle defines them the same way).
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <limits>
 
@@ -303,6 +305,9 @@ int64_t DyMuPathPlanner::localPropagation(base::Waypoint start, base::Waypoint o
     L.heap.push_back({key(p), L.seq[p], p});
     std::push_heap(L.heap.begin(), L.heap.end(), later);
   };
+  // :685-696: give up (NULL) once the propagation has run longer than the limit
+  const auto t_init = std::chrono::steady_clock::now();
+  uint64_t pops = 0;
   L.seq[agent] = L.next_seq++;
   L.in_band[agent] = 1;
   L.band_count = 1;
@@ -373,6 +378,16 @@ int64_t DyMuPathPlanner::localPropagation(base::Waypoint start, base::Waypoint o
         all = q >= 0 && L.state[q];  // U1
       }
       if (all) return end;
+    }
+    if (local_timeout_s_ > 0 && (++pops & 255) == 0 &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t_init).count() >
+            local_timeout_s_) {
+      std::fprintf(stderr,
+                   "computeLocalPropagation: ERROR: no set node after %.3g s (local narrowband "
+                   "%llu, propagated nodes %llu)\n",
+                   local_timeout_s_, (unsigned long long)L.band_count,
+                   (unsigned long long)L.propagated.size());
+      return -1;
     }
   }
 }

@@ -336,6 +336,12 @@ int dymu_planner_expand_risk(dymu_planner* p) {
   return guarded([&] { p->pl.expandRisk(); return DYMU_OK; });
 }
 
+int dymu_planner_set_local_timeout(dymu_planner* p, double seconds) {
+  if (!p) return DYMU_ERR_ARG;
+  p->pl.setLocalPropagationTimeout(seconds);
+  return DYMU_OK;
+}
+
 int dymu_planner_compute_local_propagation(dymu_planner* p, const double* s, const double* o,
                                            double* set_xy) {
   if (!p || !s || !o) return DYMU_ERR_ARG;

@@ -473,6 +473,7 @@ PLANNER_SYMBOLS = {
     "dymu_planner_evaluate_path": (_i32, [_vp, _u32]),
     "dymu_planner_expand_risk": (_i32, [_vp]),
     "dymu_planner_compute_local_propagation": (_i32, [_vp, _dp, _dp, _dp]),
+    "dymu_planner_set_local_timeout": (_i32, [_vp, ctypes.c_double]),
     "dymu_planner_get_risk_matrix": (_i32, [_vp, _d, _d, _d, _d, _dp]),
     "dymu_planner_get_deviation_matrix": (_i32, [_vp, _d, _d, _d, _d, _dp]),
     "dymu_planner_get_reconnecting_index": (_i32, [_vp]),
@@ -719,6 +720,10 @@ class Planner:
 
     def expandRisk(self):
         _check(self._lib.dymu_planner_expand_risk(self.h))
+
+    def setLocalPropagationTimeout(self, seconds: float):
+        """computeLocalPropagation's wall-clock limit (reference: 5 s, <= 0: none)."""
+        _check(self._lib.dymu_planner_set_local_timeout(self.h, float(seconds)))
 
     def computeLocalPropagation(self, w_init, w_overtake):
         """The set node's global pose (x, y), or None."""

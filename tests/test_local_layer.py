@@ -181,6 +181,20 @@ def test_node_level_access(dymu, oracle):
     assert np.isinf(p.getGlobalNode(12, 12)["total_cost"])
 
 
+def test_local_propagation_wall_clock_limit(dymu, oracle):
+    """src/DyMu_LocalPathRepairing.cpp:685-696: past the time limit the local
+    propagation gives up and returns NULL; without one it finds the set node."""
+    N = 24
+    p, o = build(dymu, oracle, N, 0.25, 0, goal=(12, 12))
+    ref = p.computeLocalPropagation((5.0, 5.0), (9.0, 9.0))
+    assert ref is not None
+    p.setLocalPropagationTimeout(1e-9)  # checked every 256 settled sub-cells
+    assert p.computeLocalPropagation((5.0, 5.0), (9.0, 9.0)) is None
+    p.setLocalPropagationTimeout(0)  # disabled
+    assert p.computeLocalPropagation((5.0, 5.0), (9.0, 9.0)) == ref
+    p.setLocalPropagationTimeout(5.0)
+
+
 @pytest.mark.parametrize("name,approach", [("cons", 0), ("sweep", 1)])
 def test_local_golden_terrain(dymu, oracle, name, approach):
     """The committed local-layer fixtures (tests/golden/gen_golden_local.py):
