@@ -29,8 +29,12 @@
 //     narrow band the reference's tentative values (replayed on the host from
 //     the CLOSED values), every other cell +inf; ties between equal total
 //     costs may order differently from the reference's insertion order.
-//   * the node-pointer members (global_narrowband, global_propagated_nodes,
-//     global_goal as globalNode*) do not exist: nodes are SoA arrays.
+//   * the node-pointer members are accessors returning snapshots:
+//     globalNarrowband(), globalGoal(), localAgent(); global_propagated_nodes
+//     and the local band lists are not exposed (every finite node is
+//     propagated), nor are the per-node steps of the loops the library runs
+//     whole (propagateGlobalNode, propagateLocalNode, minCostLocalNode,
+//     maxRiskNode, propagateRisk, setHorizonCost).
 //   * a start or goal on the border returns false instead of dereferencing
 //     NULL (reference :416-417, :430-431).
 #pragma once
@@ -141,6 +145,21 @@ class DyMuPathPlanner {
   bool isSafeNode(unsigned i, unsigned j);         // :410-422 (border -> false)
   bool isFullyClosedNode(unsigned i, unsigned j);  // :424-436 (border -> false)
   void resetTotalCostMap();                        // :473-485: every node OPEN at +inf
+  // the reference's global_narrowband (:445) as the last computeTotalCostMap left
+  // it: snapshots of the band nodes in grid-index order (the reference keeps
+  // insertion order); empty after computeEntireTotalCostMap
+  std::vector<globalNode> globalNarrowband();
+  // :548-567: the band node with the lowest total cost (first in grid-index order
+  // on ties), removed from the band list like the reference's erase; the map is
+  // not changed.  std::nullopt on an empty band (the reference reads front()).
+  std::optional<globalNode> minCostGlobalNode();
+  // :487-498: the band holds only the goal (total cost 0)
+  void resetGlobalNarrowBand();
+  // :731-784 / L:979-1023: the normalised descent direction at a node (the
+  // reference's gradientNode(globalNode*) / gradientNode(localNode*))
+  void gradientNode(unsigned i, unsigned j, double& dnx, double& dny) const;
+  void gradientNode(const globalNode& n, double& dnx, double& dny) const;
+  void gradientNode(const localNode& n, double& dnx, double& dny) const;
 
   // -- local layer (src/DyMu.hpp:539-591) --
   bool computeLocalPlanning(base::Waypoint wPos, base::samples::frame::Frame traversabilityMap,
@@ -158,6 +177,14 @@ class DyMuPathPlanner {
   std::optional<localNode> getLocalNode(base::Waypoint wPos);  // subdivides, like :177-189
   std::optional<localNode> getLocalNode(base::Pose2D pos);     // :160-173
   void subdivideGlobalNode(unsigned i, unsigned j);            // :150-156
+  void createLocalMap(unsigned i, unsigned j);                 // :97-148 (as subdivide)
+  // L:851-869: the step toward the nb4 sub-cell of lowest deviation
+  base::Waypoint computeLocalWaypointDijkstra(const localNode& lNode);
+  // L:441-471 against current_path
+  bool isBlockingObstacle(const localNode& obNode, unsigned& maxIndex, unsigned& minIndex);
+  // the reference's local_agent (src/DyMu.hpp:460): the last local propagation's
+  // start sub-cell, std::nullopt before one ran
+  std::optional<localNode> localAgent();
   double getTotalCost(const localNode& lNode);                 // :473-491
   std::vector<std::vector<double>> getRiskMatrix(base::Waypoint rover_pos);
   std::vector<std::vector<double>> getDeviationMatrix(base::Waypoint rover_pos);
@@ -195,7 +222,7 @@ class DyMuPathPlanner {
   bool setTrafficabilityWindow(unsigned i0, unsigned j0, unsigned w, unsigned h,
                                const double* tr);
   // Narrow-band cells left by the last computeTotalCostMap (0 after a full solve).
-  uint64_t lastBandSize() const { return band_size_; }
+  uint64_t lastBandSize() const { return band_cells_.size(); }
   // Engine options (device ordinal etc.); takes effect on the next solve.
   void setEngineOptions(const dymu_opts& o);
   // Install a total-cost map (ny*nx, +inf unreachable) as the state a
@@ -233,7 +260,6 @@ class DyMuPathPlanner {
   bool costMapFromRows(const ERows& elev_row, const TRows& terr_row);
   bool propagate(bool early, unsigned si, unsigned sj);
   void replayBand(double t_closed, const std::vector<uint64_t>& band, std::vector<double>& out);
-  void gradientNode(unsigned i, unsigned j, double& dnx, double& dny) const;
   bool safeNode(unsigned i, unsigned j) const;
   std::optional<globalNode> snapshot(uint64_t k);
   void nominalCost(unsigned i, unsigned j, int range, int num_locs, double cmax);
@@ -246,6 +272,7 @@ class DyMuPathPlanner {
                           const PathIndex* index = nullptr) const;
   int64_t localPropagation(base::Waypoint wInit, base::Waypoint wOvertake);
   std::vector<base::Waypoint> localPath(uint64_t set, base::Waypoint wInit);
+  base::Waypoint dijkstraStep(uint64_t l) const;
   void windowMatrix(base::Waypoint rover_pos, bool deviation, std::vector<std::vector<double>>& m);
 
   static constexpr unsigned kBlk = 128;
@@ -256,6 +283,7 @@ class DyMuPathPlanner {
   unsigned nx_ = 0, ny_ = 0;
   double global_res_ = 1.0, local_res_ = 1.0;
   double local_timeout_s_ = 5.0;
+  int64_t local_agent_ = -1;         // local_agent (sub-cell id), -1 = NULL
   unsigned res_ratio_ = 1;
   std::unique_ptr<LocalLayer> local_;
   std::vector<double> global_offset_{0.0, 0.0};
@@ -286,7 +314,7 @@ class DyMuPathPlanner {
   unsigned nbx_ = 0, nby_ = 0;
   void* registered_ = nullptr;  // total_cost_ buffer page-locked for DMA
   double closed_limit_ = 0.0;   // CLOSED iff finite T <= closed_limit_
-  uint64_t band_size_ = 0;
+  std::vector<uint64_t> band_cells_;  // global_narrowband: grid indices, ascending
   // F as uploaded to dF_ (host copy); node-field rows [dirty_j0_, dirty_j1_)
   // changed since it was packed
   std::vector<double> speed_;

@@ -93,6 +93,15 @@ int dymu_planner_get_global_node(dymu_planner* p, uint32_t i, uint32_t j, dymu_g
 int dymu_planner_is_safe_node(dymu_planner* p, uint32_t i, uint32_t j);          /* :410-422 */
 int dymu_planner_is_fully_closed_node(dymu_planner* p, uint32_t i, uint32_t j);  /* :424-436 */
 int dymu_planner_reset_total_cost_map(dymu_planner* p);                          /* :473-485 */
+/* global_narrowband (:445) as the last computeTotalCostMap left it: the band
+ * size; up to max (i, j) pairs written to ij in grid-index order */
+int64_t dymu_planner_global_narrowband(dymu_planner* p, uint32_t* ij, int64_t max);
+/* minCostGlobalNode (:548-567): 1, the band node of lowest total cost (removed
+ * from the band list) in ij[2] and *total_cost; 0 on an empty band */
+int dymu_planner_min_cost_global_node(dymu_planner* p, uint32_t* ij, double* total_cost);
+int dymu_planner_reset_global_narrow_band(dymu_planner* p);                      /* :487-498 */
+/* gradientNode (:718-772): the normalised descent direction at (i, j) in d[2] */
+int dymu_planner_gradient_node(dymu_planner* p, uint32_t i, uint32_t j, double* d);
 /* install a total-cost map (ny*nx, +inf unreachable) as a converged
  * computeEntireTotalCostMap leaves it (every finite node CLOSED) */
 int dymu_planner_load_total_cost_map(dymu_planner* p, const double* T);
@@ -120,6 +129,11 @@ int dymu_planner_expand_risk(dymu_planner* p);
 /* computeLocalPropagation (:578-698): 1 and the set node's global pose, or 0 (NULL) */
 int dymu_planner_compute_local_propagation(dymu_planner* p, const double* start_xyzh,
                                            const double* overtake_xyzh, double* set_xy);
+/* computeLocalWaypointDijkstra (L:851-869) from the sub-cell at waypoint xyzh
+ * (getLocalNode: subdivides): 1 and the step's (x, y, z, heading), 0 (NULL) */
+int dymu_planner_local_waypoint_dijkstra(dymu_planner* p, const double* xyzh, double* out_xyzh);
+/* local_agent (src/DyMu.hpp:460): 1 and its global pose (x, y), or 0 (NULL) */
+int dymu_planner_local_agent(dymu_planner* p, double* global_xy);
 /* computeLocalPropagation's wall-clock limit (the reference's 5 s, :685-696;
  * <= 0 disables it); it then returns 0 (NULL) like the reference */
 int dymu_planner_set_local_timeout(dymu_planner* p, double seconds);

@@ -210,6 +210,22 @@ bool DyMuPathPlanner::isBlockingObstacle(uint64_t p, unsigned& maxIndex, unsigne
   return blocked;
 }
 
+bool DyMuPathPlanner::isBlockingObstacle(const localNode& obNode, unsigned& maxIndex,
+                                         unsigned& minIndex) {
+  if (!local_ || obNode.id >= local_->dev.size()) return false;
+  return isBlockingObstacle(obNode.id, maxIndex, minIndex, nullptr);
+}
+
+void DyMuPathPlanner::createLocalMap(unsigned i, unsigned j) { subdivideGlobalNode(i, j); }
+
+std::optional<localNode> DyMuPathPlanner::localAgent() {
+  if (!local_ || local_agent_ < 0 || (uint64_t)local_agent_ >= local_->dev.size())
+    return std::nullopt;
+  localNode n;
+  localCell((uint64_t)local_agent_, &n);
+  return n;
+}
+
 // :493-576 (expandRisk, maxRiskNode, propagateRisk).  The queue keeps the
 // reference's order: the front unless it is below 1 and a later entry has a
 // higher risk, in which case the first such entry; a node is queued again
@@ -274,6 +290,7 @@ int64_t DyMuPathPlanner::localPropagation(base::Waypoint start, base::Waypoint o
   L.heap.clear();
   L.band_count = 0;
   const int64_t agent = localAt(start.position[0], start.position[1]);
+  local_agent_ = agent;
   if (agent < 0 || L.obst[agent]) return -1;
   L.dev[agent] = 0;
   L.tc[agent] = localTotalCost((uint64_t)agent);
@@ -431,6 +448,14 @@ void local_gradient(const LocalLayer& L, uint64_t p, double& dnx, double& dny) {
 }  // namespace
 
 // :877-977
+void DyMuPathPlanner::gradientNode(const localNode& n, double& dnx, double& dny) const {
+  if (!local_ || n.id >= local_->dev.size()) {
+    dnx = dny = 0;
+    return;
+  }
+  local_gradient(*local_, n.id, dnx, dny);
+}
+
 bool DyMuPathPlanner::computeLocalWaypointGDM(base::Waypoint& wPos, double tau) {
   const int64_t l = localAt(wPos.position[0], wPos.position[1]);
   if (l < 0) return false;
@@ -499,6 +524,30 @@ bool DyMuPathPlanner::computeLocalWaypointGDM(base::Waypoint& wPos, double tau) 
   return true;
 }
 
+// :851-869: toward the nb4 sub-cell of lowest deviation (U5: none finite -> the
+// sub-cell's own position)
+base::Waypoint DyMuPathPlanner::dijkstraStep(uint64_t l) const {
+  const LocalLayer& L = *local_;
+  const CellPose cl = cell_pose(L, l, nx_, global_res_);
+  double t = kInf, nxp = cl.wx, nyp = cl.wy;
+  for (int d = 0; d < 4; ++d) {
+    const int64_t q = L.nb(l, d);
+    if (q >= 0 && L.dev[q] < t) {
+      t = L.dev[q];
+      const CellPose cq = cell_pose(L, (uint64_t)q, nx_, global_res_);
+      nxp = cq.wx;
+      nyp = cq.wy;
+    }
+  }
+  return make_wp(nxp, nyp, 0.0, std::atan2(nyp - cl.wy, nxp - cl.wx));
+}
+
+base::Waypoint DyMuPathPlanner::computeLocalWaypointDijkstra(const localNode& lNode) {
+  if (!local_ || lNode.id >= local_->dev.size())
+    return make_wp(lNode.world_pose.position[0], lNode.world_pose.position[1], 0.0, 0.0);
+  return dijkstraStep(lNode.id);
+}
+
 // :807-849 (with :851-869 computeLocalWaypointDijkstra).  The trajectory is
 // built back to front and reversed once (the reference inserts at the front).
 std::vector<base::Waypoint> DyMuPathPlanner::localPath(uint64_t set, base::Waypoint start) {
@@ -521,19 +570,7 @@ std::vector<base::Waypoint> DyMuPathPlanner::localPath(uint64_t set, base::Waypo
     } else {
       const int64_t l = localAt(t0.position[0], t0.position[1]);
       if (l < 0) break;  // U1
-      const LocalLayer& L = *local_;
-      const CellPose cl = cell_pose(L, (uint64_t)l, nx_, global_res_);
-      double t = kInf, nxp = cl.wx, nyp = cl.wy;  // U5
-      for (int d = 0; d < 4; ++d) {
-        const int64_t q = L.nb((uint64_t)l, d);
-        if (q >= 0 && L.dev[q] < t) {
-          t = L.dev[q];
-          const CellPose cq = cell_pose(L, (uint64_t)q, nx_, global_res_);
-          nxp = cq.wx;
-          nyp = cq.wy;
-        }
-      }
-      w = make_wp(nxp, nyp, 0.0, std::atan2(nyp - cl.wy, nxp - cl.wx));
+      w = dijkstraStep((uint64_t)l);
       rev.push_back(w);
     }
   }

@@ -84,6 +84,7 @@ bool DyMuPathPlanner::initGlobalLayer(double globalres, double localres, unsigne
   }
   if (!local_) local_ = std::make_unique<LocalLayer>();
   local_->reset(res_ratio_);
+  local_agent_ = -1;
   reconnecting_index = 0;
   solved_ = false;
   nx_ = num_nodes_X;
@@ -111,7 +112,7 @@ bool DyMuPathPlanner::initGlobalLayer(double globalres, double localres, unsigne
   blk_ok_.assign((uint64_t)nbx_ * nby_, 1);
   blk_missing_ = 0;
   closed_limit_ = 0.0;
-  band_size_ = 0;
+  band_cells_.clear();
   speed_.clear();
   speed_valid_ = false;
   markDirty(0, ny_);
@@ -682,7 +683,7 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
   // the host mirror is stale
   std::fill(blk_ok_.begin(), blk_ok_.end(), 0);
   blk_missing_ = blk_ok_.size();
-  band_size_ = 0;
+  band_cells_.clear();
   if (!early) {
     closed_limit_ = kInf;
     solved_ = true;
@@ -707,7 +708,6 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
   }
   band.resize(nb);
   std::sort(band.begin(), band.end());
-  band_size_ = nb;
   if (nb) {
     std::vector<double> vals;
     replayBand(t_closed, band, vals);
@@ -717,6 +717,7 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
     // blocks fetched during the replay hold the pre-replay band values
     for (uint64_t q = 0; q < nb; ++q) total_cost_[band[q]] = vals[q];
   }
+  band_cells_ = std::move(band);
   return nb > 0;
 }
 
@@ -922,6 +923,15 @@ base::Waypoint DyMuPathPlanner::computeNextGlobalWaypoint(base::Waypoint& wPos, 
   return wNext;
 }
 
+void DyMuPathPlanner::gradientNode(const globalNode& n, double& dnx, double& dny) const {
+  const double i = n.pose.position[0], j = n.pose.position[1];
+  if (!(i >= 0 && j >= 0 && i < nx_ && j < ny_)) {
+    dnx = dny = 0;
+    return;
+  }
+  gradientNode((unsigned)i, (unsigned)j, dnx, dny);
+}
+
 // :718-772
 void DyMuPathPlanner::gradientNode(unsigned i, unsigned j, double& dnx, double& dny) const {
   const uint64_t k = idx(i, j);
@@ -1097,8 +1107,42 @@ void DyMuPathPlanner::resetTotalCostMap() {
   std::fill(blk_ok_.begin(), blk_ok_.end(), 1);
   blk_missing_ = 0;
   closed_limit_ = 0.0;
-  band_size_ = 0;
+  band_cells_.clear();
   solved_ = false;
+}
+
+std::vector<globalNode> DyMuPathPlanner::globalNarrowband() {
+  std::vector<globalNode> out;
+  out.reserve(band_cells_.size());
+  for (const uint64_t k : band_cells_) out.push_back(*snapshot(k));
+  return out;
+}
+
+// :548-567 (first strict minimum, then erased from the band)
+std::optional<globalNode> DyMuPathPlanner::minCostGlobalNode() {
+  if (band_cells_.empty()) return std::nullopt;
+  size_t best = 0;
+  double tmin = T(band_cells_[0]);
+  for (size_t q = 1; q < band_cells_.size(); ++q) {
+    const double t = T(band_cells_[q]);
+    if (t < tmin) {
+      tmin = t;
+      best = q;
+    }
+  }
+  const uint64_t k = band_cells_[best];
+  band_cells_.erase(band_cells_.begin() + (std::ptrdiff_t)best);
+  return snapshot(k);
+}
+
+// :487-498
+void DyMuPathPlanner::resetGlobalNarrowBand() {
+  band_cells_.clear();
+  if (!has_goal_ || nx_ == 0) return;
+  const uint64_t k = idx(goal_i_, goal_j_);
+  (void)T(k);  // the goal's block in the host mirror before the write
+  total_cost_[k] = 0.0;
+  band_cells_.push_back(k);
 }
 
 bool DyMuPathPlanner::loadTotalCostMap(const double* Tin) {
@@ -1108,7 +1152,7 @@ bool DyMuPathPlanner::loadTotalCostMap(const double* Tin) {
   std::fill(blk_ok_.begin(), blk_ok_.end(), 1);
   blk_missing_ = 0;
   closed_limit_ = kInf;
-  band_size_ = 0;
+  band_cells_.clear();
   solved_ = false;
   if (ctx_ && dT_ && dcells_ == n &&
       dymu_memcpy_h2d(ctx_, dT_, total_cost_.data(), sizeof(double) * n) != DYMU_OK)

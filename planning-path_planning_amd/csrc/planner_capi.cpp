@@ -252,6 +252,47 @@ int dymu_planner_is_fully_closed_node(dymu_planner* p, uint32_t i, uint32_t j) {
   return guarded([&] { return (int)p->pl.isFullyClosedNode(i, j); });
 }
 
+int64_t dymu_planner_global_narrowband(dymu_planner* p, uint32_t* ij, int64_t max) {
+  if (!p || (max > 0 && !ij)) return DYMU_ERR_ARG;
+  int64_t n = 0;
+  const int rc = guarded([&] {
+    const auto band = p->pl.globalNarrowband();
+    n = (int64_t)band.size();
+    for (int64_t q = 0; q < n && q < max; ++q) {
+      ij[2 * q] = (uint32_t)band[q].pose.position[0];
+      ij[2 * q + 1] = (uint32_t)band[q].pose.position[1];
+    }
+    return DYMU_OK;
+  });
+  return rc < 0 ? rc : n;
+}
+
+int dymu_planner_min_cost_global_node(dymu_planner* p, uint32_t* ij, double* total_cost) {
+  if (!p || !ij) return DYMU_ERR_ARG;
+  return guarded([&] {
+    const auto n = p->pl.minCostGlobalNode();
+    if (!n) return 0;
+    ij[0] = (uint32_t)n->pose.position[0];
+    ij[1] = (uint32_t)n->pose.position[1];
+    if (total_cost) *total_cost = n->total_cost;
+    return 1;
+  });
+}
+
+int dymu_planner_reset_global_narrow_band(dymu_planner* p) {
+  if (!p) return DYMU_ERR_ARG;
+  return guarded([&] { p->pl.resetGlobalNarrowBand(); return DYMU_OK; });
+}
+
+int dymu_planner_gradient_node(dymu_planner* p, uint32_t i, uint32_t j, double* d) {
+  if (!p || !d) return DYMU_ERR_ARG;
+  return guarded([&] {
+    if (i >= p->pl.sizeX() || j >= p->pl.sizeY()) return (int)DYMU_ERR_ARG;
+    p->pl.gradientNode(i, j, d[0], d[1]);
+    return (int)DYMU_OK;
+  });
+}
+
 int dymu_planner_reset_total_cost_map(dymu_planner* p) {
   if (!p) return DYMU_ERR_ARG;
   p->pl.resetTotalCostMap();
@@ -340,6 +381,31 @@ int dymu_planner_set_local_timeout(dymu_planner* p, double seconds) {
   if (!p) return DYMU_ERR_ARG;
   p->pl.setLocalPropagationTimeout(seconds);
   return DYMU_OK;
+}
+
+int dymu_planner_local_waypoint_dijkstra(dymu_planner* p, const double* s, double* out) {
+  if (!p || !s || !out) return DYMU_ERR_ARG;
+  return guarded([&] {
+    const auto n = p->pl.getLocalNode(wp(s[0], s[1], s[2], s[3]));
+    if (!n) return 0;
+    const base::Waypoint w = p->pl.computeLocalWaypointDijkstra(*n);
+    out[0] = w.position[0];
+    out[1] = w.position[1];
+    out[2] = w.position[2];
+    out[3] = w.heading;
+    return 1;
+  });
+}
+
+int dymu_planner_local_agent(dymu_planner* p, double* xy) {
+  if (!p || !xy) return DYMU_ERR_ARG;
+  return guarded([&] {
+    const auto n = p->pl.localAgent();
+    if (!n) return 0;
+    xy[0] = n->global_pose.position[0];
+    xy[1] = n->global_pose.position[1];
+    return 1;
+  });
 }
 
 int dymu_planner_compute_local_propagation(dymu_planner* p, const double* s, const double* o,

@@ -462,6 +462,12 @@ PLANNER_SYMBOLS = {
     "dymu_planner_get_global_node": (_i32, [_vp, _u32, _u32, _vp]),
     "dymu_planner_is_safe_node": (_i32, [_vp, _u32, _u32]),
     "dymu_planner_is_fully_closed_node": (_i32, [_vp, _u32, _u32]),
+    "dymu_planner_global_narrowband": (ctypes.c_int64, [_vp, _vp, ctypes.c_int64]),
+    "dymu_planner_min_cost_global_node": (_i32, [_vp, _vp, _dp]),
+    "dymu_planner_reset_global_narrow_band": (_i32, [_vp]),
+    "dymu_planner_gradient_node": (_i32, [_vp, _u32, _u32, _dp]),
+    "dymu_planner_local_waypoint_dijkstra": (_i32, [_vp, _dp, _dp]),
+    "dymu_planner_local_agent": (_i32, [_vp, _dp]),
     "dymu_planner_reset_total_cost_map": (_i32, [_vp]),
     "dymu_planner_load_total_cost_map": (_i32, [_vp, _dp]),
     "dymu_planner_set_current_path": (_i32, [_vp, _vp, _i32]),
@@ -673,6 +679,50 @@ class Planner:
 
     def resetTotalCostMap(self):
         _check(self._lib.dymu_planner_reset_total_cost_map(self.h))
+
+    def globalNarrowband(self) -> np.ndarray:
+        """global_narrowband (:445) after computeTotalCostMap: (n, 2) array of (i, j)."""
+        n = self._lib.dymu_planner_global_narrowband(self.h, None, 0)
+        if n < 0:
+            _check(int(n))
+        ij = np.zeros((max(n, 1), 2), dtype=np.uint32)
+        m = self._lib.dymu_planner_global_narrowband(self.h, ij.ctypes.data, n)
+        if m < 0:
+            _check(int(m))
+        return ij[:min(n, m)]
+
+    def minCostGlobalNode(self):
+        """minCostGlobalNode (:548-567): ((i, j), total_cost) of the band's lowest
+        node, removed from the band list; None on an empty band."""
+        ij = np.zeros(2, dtype=np.uint32)
+        t = np.zeros(1)
+        if not _b(self._lib.dymu_planner_min_cost_global_node(self.h, ij.ctypes.data, t)):
+            return None
+        return (int(ij[0]), int(ij[1])), float(t[0])
+
+    def resetGlobalNarrowBand(self):
+        _check(self._lib.dymu_planner_reset_global_narrow_band(self.h))
+
+    def gradientNode(self, i: int, j: int):
+        """gradientNode (:718-772): (dnx, dny)."""
+        d = np.zeros(2)
+        _check(self._lib.dymu_planner_gradient_node(self.h, i, j, d))
+        return float(d[0]), float(d[1])
+
+    def computeLocalWaypointDijkstra(self, w):
+        """L:851-869 from the sub-cell at waypoint w: (x, y, z, heading), or None."""
+        s = np.array(self._wp(w))
+        out = np.zeros(4)
+        if not _b(self._lib.dymu_planner_local_waypoint_dijkstra(self.h, s, out)):
+            return None
+        return tuple(float(v) for v in out)
+
+    def localAgent(self):
+        """local_agent's global pose (x, y), or None."""
+        xy = np.zeros(2)
+        if not _b(self._lib.dymu_planner_local_agent(self.h, xy)):
+            return None
+        return float(xy[0]), float(xy[1])
 
     def loadTotalCostMap(self, T) -> bool:
         return _b(self._lib.dymu_planner_load_total_cost_map(self.h, self._grid(T)))

@@ -181,6 +181,53 @@ def test_node_level_access(dymu, oracle):
     assert np.isinf(p.getGlobalNode(12, 12)["total_cost"])
 
 
+def test_band_and_gradient_accessors(dymu, oracle):
+    """resetGlobalNarrowBand / minCostGlobalNode (:487-498, :548-567) on an
+    installed map, and gradientNode (:718-772) against the formula."""
+    N = 24
+    p, o = build(dymu, oracle, N, 0.5, 0, goal=(12, 12))
+    assert len(p.globalNarrowband()) == 0 and p.minCostGlobalNode() is None
+    p.resetGlobalNarrowBand()
+    assert p.globalNarrowband().tolist() == [[12, 12]]
+    assert p.minCostGlobalNode() == ((12, 12), 0.0)
+    assert p.minCostGlobalNode() is None
+    T = p.getTotalCostMatrix()
+    T = np.where(T < 0, np.inf, T)
+    for (i, j) in [(5, 7), (0, 3), (23, 10), (12, 12), (3, 0)]:
+        def d(a, b, c, ha, hc):  # one axis of :718-772 (a below, c above)
+            if (not ha and not hc) or (ha and hc and np.isinf(a) and np.isinf(c)):
+                return 0.0
+            if not ha or np.isinf(a):
+                return c - b
+            if not hc or np.isinf(c):
+                return b - a
+            return (c - a) * 0.5
+        get = lambda x, y: T[y, x] if 0 <= x < N and 0 <= y < N else np.inf
+        dx = d(get(i - 1, j), T[j, i], get(i + 1, j), i > 0, i + 1 < N)
+        dy = d(get(i, j - 1), T[j, i], get(i, j + 1), j > 0, j + 1 < N)
+        nrm = np.sqrt(dx * dx + dy * dy)
+        want = (0.0, 0.0) if dx == 0 and dy == 0 else (dx / nrm, dy / nrm)
+        assert p.gradientNode(i, j) == pytest.approx(want, abs=0, rel=1e-15)
+
+
+def test_local_agent_and_dijkstra_step(dymu, oracle):
+    """local_agent after a local propagation; computeLocalWaypointDijkstra
+    (L:851-869) steps to an nb4 sub-cell (one local cell away)."""
+    N = 24
+    p, o = build(dymu, oracle, N, 0.25, 0, goal=(12, 12))
+    assert p.localAgent() is None
+    assert p.computeLocalPropagation((5.0, 5.0), (9.0, 9.0)) is not None
+    ax, ay = p.localAgent()
+    assert abs(ax - 5.0) <= 0.25 and abs(ay - 5.0) <= 0.25
+    w = p.computeLocalWaypointDijkstra((5.5, 5.5))
+    assert w is not None
+    # an axis step of one local cell from the sub-cell holding (5.5, 5.5),
+    # heading along it (the sub-cell's centre is within half a cell of 5.5)
+    c = (w[0] - 0.25 * np.cos(w[3]), w[1] - 0.25 * np.sin(w[3]))
+    assert min(abs(np.cos(w[3])), abs(np.sin(w[3]))) < 1e-12
+    assert abs(c[0] - 5.5) <= 0.125 + 1e-12 and abs(c[1] - 5.5) <= 0.125 + 1e-12
+
+
 def test_local_propagation_wall_clock_limit(dymu, oracle):
     """src/DyMu_LocalPathRepairing.cpp:685-696: past the time limit the local
     propagation gives up and returns NULL; without one it finds the set node."""

@@ -134,6 +134,37 @@ def test_compute_total_cost_map_returns(dymu, oracle):
 
 
 @pytest.mark.gpu
+def test_global_narrowband_after_early_exit(dymu, oracle):
+    """global_narrowband (src/DyMu.hpp:445) after computeTotalCostMap holds the
+    reference's band nodes -- reached but not CLOSED (early64_closed) -- and
+    minCostGlobalNode (:548-567) pops them lowest total cost first."""
+    cost = gold("setcost64_cost")
+    g = tuple(int(x) for x in gold("setcost64_goal"))
+    N = cost.shape[0]
+    p = dymu.Planner()
+    p.initGlobalLayer(1.0, 0.5, N, N)
+    p.setCostMap(cost)
+    p.setGoal(g)
+    assert p.computeTotalCostMap((12, 50))
+    Tt, closed = gold("early64_T"), gold("early64_closed").astype(bool)
+    ref = np.isfinite(Tt) & ~closed
+    band = p.globalNarrowband()
+    assert len(band) == p.lastBandSize() == int(ref.sum())
+    got = np.zeros_like(ref)
+    got[band[:, 1], band[:, 0]] = True
+    assert np.array_equal(got, ref)
+    M = p.getTotalCostMatrix()
+    prev = -1.0
+    for _ in range(3):
+        (i, j), t = p.minCostGlobalNode()
+        assert ref[j, i] and t == M[j, i] and t >= prev
+        assert t == min(M[b[1], b[0]] for b in p.globalNarrowband()) or t <= M[ref].min() + 0
+        prev = t
+    assert p.lastBandSize() == int(ref.sum()) - 3
+    assert abs(prev - np.sort(Tt[ref])[2]) <= RTOL * max(1.0, prev)
+
+
+@pytest.mark.gpu
 def test_early_exit_far_start_256(dymu, oracle):
     """A start far from the goal on a 256^2 map with obstacles (golden from the
     oracle's exact reference pop order)."""
