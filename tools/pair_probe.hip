@@ -27,6 +27,36 @@ __device__ __forceinline__ void rb_update1(const double* p, const double* pn, co
   t = vmin64(t, u);
 }
 
+// kernel 5's rb_update2 on two tiles at once (4 cells, two per tile): every
+// neighbour read in flight before one wait, then the four chains interleaved
+__device__ __forceinline__ void rb_update4(const double* p, const double* pn, const double* ps,
+                                           const double* q, const double* qn, const double* qs,
+                                           const double (&f)[4], double (&t)[4], bool (&ch)[4]) {
+  double w[4] = {p[-1], p[1], q[-1], q[1]}, e[4] = {p[1], p[3], q[1], q[3]};
+  double n[4] = {pn[0], pn[2], qn[0], qn[2]}, so[4] = {ps[0], ps[2], qs[0], qs[2]};
+  asm volatile("" : "+v"(w[0]), "+v"(e[0]), "+v"(n[0]), "+v"(so[0]), "+v"(w[1]), "+v"(e[1]),
+               "+v"(n[1]), "+v"(so[1]));
+  asm volatile("" : "+v"(w[2]), "+v"(e[2]), "+v"(n[2]), "+v"(so[2]), "+v"(w[3]), "+v"(e[3]),
+               "+v"(n[3]), "+v"(so[3]));
+  double c2[4], tx[4], ty[4], m[4], d[4], v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    c2[k] = 2.0 * (f[k] * f[k]);
+    tx[k] = vmin64(w[k], e[k]);
+    ty[k] = vmin64(n[k], so[k]);
+    m[k] = vmin64(tx[k], ty[k]);
+    d[k] = tx[k] - ty[k];
+  }
+  two_sided_approx2(ty[0], d[0], c2[0], ty[1], d[1], c2[1], v[0], v[1]);
+  two_sided_approx2(ty[2], d[2], c2[2], ty[3], d[3], c2[3], v[2], v[3]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double u = fabs(d[k]) < f[k] ? v[k] : m[k] + f[k];
+    ch[k] = u < t[k];
+    t[k] = vmin64(t[k], u);
+  }
+}
+
 // pair barrier: publish v, wait for the partner's arrival, return its v
 struct Pair {
   uint32_t* cnt;  // [2]
@@ -55,7 +85,46 @@ __global__ __launch_bounds__(1024) void k_probe(double* sink, uint32_t* err, int
   __shared__ double s_img[16][IMG16];
   __shared__ uint32_t s_cnt[8][2], s_pw[8][4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (MODE == 0) {
+  if (MODE == 2) {  // two tiles per wave (waves <= 8: two images each)
+    double* imgA = s_img[2 * wv];
+    double* imgB = s_img[2 * wv + 1];
+    for (int k = lane; k < IMG16; k += 64) {
+      imgA[k] = 1000.0 + (double)((k * 37) % 101);
+      imgB[k] = 1000.0 + (double)((k * 41) % 103);
+    }
+    const int r = lane >> 2, q = lane & 3, odd = r & 1;
+    const int rb = img16_row(r);
+    const int dn = img16_row(r + 1) - rb, ds = rb - img16_row(r - 1);
+    double* prA = imgA + rb + 4 * q + odd;
+    double* pbA = imgA + rb + 4 * q + 1 - odd;
+    double* prB = imgB + rb + 4 * q + odd;
+    double* pbB = imgB + rb + 4 * q + 1 - odd;
+    const double fr[4] = {1.5 + 0.01 * lane, 2.5, 1.75, 2.25 + 0.01 * lane};
+    const double fb[4] = {3.0, 1.25 + 0.02 * lane, 2.0 + 0.01 * lane, 1.5};
+    double tr[4] = {prA[0], prA[2], prB[0], prB[2]}, tb[4] = {pbA[0], pbA[2], pbB[0], pbB[2]};
+    bool cr[4], cb[4];
+    int any = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (int s = 0; s < pairs; ++s) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        __builtin_amdgcn_wave_barrier();
+        rb_update4(prA, prA + dn, prA - ds, prB, prB + dn, prB - ds, fr, tr, cr);
+        prA[0] = tr[0];
+        prA[2] = tr[1];
+        prB[0] = tr[2];
+        prB[2] = tr[3];
+        __builtin_amdgcn_wave_barrier();
+        rb_update4(pbA, pbA + dn, pbA - ds, pbB, pbB + dn, pbB - ds, fb, tb, cb);
+        pbA[0] = tb[0];
+        pbA[2] = tb[1];
+        pbB[0] = tb[2];
+        pbB[2] = tb[3];
+      }
+      any += __any(cr[0] || cr[1] || cr[2] || cr[3] || cb[0] || cb[1] || cb[2] || cb[3]) ? 1 : 0;
+    }
+    sink[blockIdx.x * blockDim.x + threadIdx.x] = tr[0] + tr[1] + tr[2] + tr[3] + tb[0] + tb[1] + tb[2] + tb[3] + any;
+  } else if (MODE == 0) {
     double* img = s_img[wv];
     for (int k = lane; k < IMG16; k += 64) img[k] = 1000.0 + (double)((k * 37) % 101);
     const int r = lane >> 2, q = lane & 3, odd = r & 1;
@@ -84,7 +153,7 @@ __global__ __launch_bounds__(1024) void k_probe(double* sink, uint32_t* err, int
       any += __any(c0 || c1 || c2 || c3) ? 1 : 0;
     }
     sink[blockIdx.x * blockDim.x + threadIdx.x] = tr[0] + tr[1] + tb[0] + tb[1] + any;
-  } else {
+  } else if (MODE == 1) {
     const int p = wv >> 1, h = wv & 1;
     double* img = s_img[p];
     if (lane < 2) s_cnt[p][lane] = 0u;
@@ -145,7 +214,7 @@ static void run(double* sink, uint32_t* err, int cus, int waves, int pairs) {
   CK(hipEventElapsedTime(&ms, a, b));
   uint32_t e = 0;
   CK(hipMemcpy(&e, err, sizeof e, hipMemcpyDeviceToHost));
-  const int tiles = M == 0 ? waves : waves / 2;
+  const int tiles = M == 0 ? waves : M == 2 ? 2 * waves : waves / 2;
   const double ns = 1e6 * ms / pairs;
   std::printf("mode %d waves/CU %2d tiles/CU %2d: %7.1f ns per tile sweep pair, %6.2f tile-pairs/us/CU%s\n",
               M, waves, tiles, ns, 1e3 * tiles / ns, e ? "  [SPIN LIMIT HIT]" : "");
@@ -165,6 +234,7 @@ int main(int argc, char** argv) {
   CK(hipMemset(err, 0, sizeof(uint32_t)));
   for (int w : {4, 8, 12, 16}) run<0>(sink, err, cus, w, pairs);
   for (int w : {2, 4, 8, 12, 16}) run<1>(sink, err, cus, w, pairs);
+  for (int w : {4, 8}) run<2>(sink, err, cus, w, pairs);
   CK(hipFree(sink));
   CK(hipFree(err));
   return 0;
