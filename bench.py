@@ -70,6 +70,8 @@ def parse():
                     help="edge of the grid the reference's linear-scan band is timed on")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the exact-sqrt / deterministic re-runs of the headline solve")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the whole-map comparison with the cpu_baseline's oracle map")
     ap.add_argument("--no-planner", action="store_true",
                     help="skip the class-surface leg (computeEntireTotalCostMap through "
                          "libdymu_planner.so)")
@@ -110,8 +112,9 @@ def host_cpu():
     return {"nproc": os.cpu_count(), "model": model}
 
 
-def cpu_baseline(n_edge, obst):
-    """Oracle heap FMM (reference pop order) on an n_edge^2 config-3 grid, 1 thread."""
+def cpu_baseline(n_edge, obst, keep=None):
+    """Oracle heap FMM (reference pop order) on an n_edge^2 config-3 grid, 1 thread.
+    keep: a dict that receives the oracle's map (keep["T"]) for the parity check."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi
 
@@ -121,6 +124,9 @@ def cpu_baseline(n_edge, obst):
     t0 = time.perf_counter()
     T, _ = o.fmm(F, g)
     dt = time.perf_counter() - t0
+    del F
+    if keep is not None:
+        keep["T"] = T
     return {
         "value": n_edge * n_edge / dt / 1e6,
         "unit": "Mcells/s",
@@ -130,6 +136,27 @@ def cpu_baseline(n_edge, obst):
                   f"FMM with the reference's pop order, 1 thread, {dt:.1f}s",
         "host": host_cpu(),
     }
+
+
+def oracle_parity(Tg, To, rtol=1e-12):
+    """The headline map against the oracle heap FMM's on the same grid (both n x n):
+    identical +inf mask, max |Tg - To| / max(1, To) over the finite cells (row blocks,
+    so the temporaries stay small)."""
+    n = Tg.shape[0]
+    worst, finite, mism = 0.0, 0, 0
+    for r0 in range(0, n, 1024):
+        a, b = Tg[r0:r0 + 1024], To[r0:r0 + 1024]
+        fa, fb = np.isfinite(a), np.isfinite(b)
+        mism += int(np.count_nonzero(fa != fb))
+        both = fa & fb
+        finite += int(np.count_nonzero(fb))
+        if both.any():
+            d = np.abs(a[both] - b[both]) / np.maximum(1.0, b[both])
+            worst = max(worst, float(d.max()))
+    return {"reference": "oracle heap FMM (the reference's propagation, ported; 1 thread) on the "
+                         "same grid, the cpu_baseline run",
+            "max_rel": worst, "finite_cells": finite, "mismatched_cells": mism, "rtol": rtol,
+            "ok": mism == 0 and worst <= rtol}
 
 
 def cpu_reference_algorithm(n_edge, obst):
@@ -224,6 +251,9 @@ def run_single(args):
     eng.set_profiling(False)
     T = np.empty(2)
     eng.d2h(T, dT)  # touch the result
+    if getattr(args, "keep_result", False):  # the last timed solve's map, for oracle parity
+        tot["T"] = np.empty((N, N))
+        eng.d2h(tot["T"], dT)
     # the same solve with the arithmetic / schedule options the headline leaves off
     # (DESIGN.md s4): the correctly rounded sweep sqrt (every update bit-identical
     # to the reference formula, :531-535) and the bit-reproducible schedule
@@ -322,6 +352,9 @@ def main():
             return
         dt, tot, kern_ms, kern_n, st = res
     else:
+        # the whole map of the last timed solve is checked against the oracle's, which
+        # the cpu_baseline leg computes on the same grid anyway
+        args.keep_result = (args.cpu_sample == args.size and not args.no_parity)
         dt, tot, kern_ms, kern_n, st = run_single(args)
     if rank != 0:
         return
@@ -453,12 +486,15 @@ def main():
             "last_solve_kind": kind,
         }
     if world == 1 and args.cpu_sample > 0 and not args.fake_cpu:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.obst)
+        keep = {} if tot.get("T") is not None else None
+        line["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.obst, keep)
+        if keep:
+            line["parity"] = oracle_parity(tot.pop("T"), keep.pop("T"))
         line["cpu_reference_algorithm"] = cpu_reference_algorithm(args.cpu_linear_size, args.obst)
         line["cpu_parallel"] = cpu_parallel(args.cpu_sample, args.obst)
     print(json.dumps(line), flush=True)
     if line.get("parity") is not None and not line["parity"]["ok"]:
-        sys.exit(f"bench: the stitched map failed its self-check: {line['parity']}")
+        sys.exit(f"bench: the map failed its parity check: {line['parity']}")
 
 
 if __name__ == "__main__":
