@@ -89,3 +89,19 @@ def test_bench_gpus2_ipc_one_gpu_self_check():
     par = rec["parity"]
     assert par["ok"] and par["ghost_max_abs_diff"] == 0 and par["mismatched_cells"] == 0
     assert par["finite_cells"] == par["finite_cells_single"] > 0.9 * 2048 * 2048
+
+
+@pytest.mark.gpu
+def test_bench_single_gpu_oracle_parity():
+    """The single-GPU bench line checks its whole map against the cpu_baseline's
+    oracle FMM map of the same grid (bench.oracle_parity) and carries the block."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--size", "1024",
+                          "--cpu-sample", "1024", "--cpu-linear-size", "256", "--steps", "2",
+                          "--warmup", "1", "--no-variants", "--no-planner"],
+                         env=_env(), cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    par = rec["parity"]
+    assert par["ok"] and par["mismatched_cells"] == 0 and par["max_rel"] <= 1e-12
+    assert par["finite_cells"] > 0.9 * 1024 * 1024
+    assert rec["cpu_baseline"]["sample"].startswith("1024x1024")
