@@ -356,6 +356,11 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   a.sweep_deadline = (variant == 5 && big) ? 1400u : 0u;  // 10-ns s_memrealtime ticks
   if (const char* kv = std::getenv("DYMU_SWEEP_DEADLINE"))
     a.sweep_deadline = (uint32_t)std::max(0, std::atoi(kv));
+  // at most 90% of the listed tiles per pass: a short list (the serpentine maze, the first
+  // passes of an open grid) is otherwise relaxed whole, and every improvement behind the
+  // front re-relaxes the tiles downstream of it; DYMU_PRIO_CAPFRAC=0: off
+  a.cap_frac = 0.9f;
+  if (const char* kv = std::getenv("DYMU_PRIO_CAPFRAC")) a.cap_frac = (float)std::atof(kv);
   a.exact_sqrt = c->opts.exact_sqrt != 0;
   if (const char* kv = std::getenv("DYMU_EXACT_SQRT")) a.exact_sqrt = std::atoi(kv) != 0;
   if (c->opts.deterministic) {

@@ -55,6 +55,7 @@ struct PassArgs {
   const double* delta;    // histogram bin width (k_prio_init)
   uint32_t target;        // tiles to relax per pass; 0 = all (plain FIM)
   float target_frac;      // ... at least this fraction of the active list
+  float cap_frac;         // kernel 5: ... and at most this fraction (>= 256 tiles); 0 = off
   int prune;              // activate a neighbour only through edge cells below its halo value
   unsigned long long* trace;  // debug: kTracePts s_memrealtime stamps per block, or null
   uint32_t sweep_deadline;  // kernel 5 (dyn): > 0: a visit stops sweeping this many 10-ns ticks

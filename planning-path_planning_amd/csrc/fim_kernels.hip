@@ -1129,7 +1129,12 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     if (lane < kShards) s_pref[lane + 1] = c;
     const uint32_t n = __shfl(c, kShards - 1);
     const uint32_t fr = (uint32_t)(a.target_frac * (float)n);
-    const uint32_t target = a.target > fr ? a.target : fr;
+    uint32_t target = a.target > fr ? a.target : fr;
+    if (a.cap_frac > 0.0f) {  // at most this fraction of the list (not below 256 tiles)
+      uint32_t cf = (uint32_t)(a.cap_frac * (float)n);
+      cf = cf > 256u ? cf : 256u;
+      target = target < cf ? target : cf;
+    }
     const unsigned long long m = __ballot(h >= target && lane < kBins - 1);
     if (lane == 0) {
       s_pref[0] = 0u;
