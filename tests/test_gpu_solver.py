@@ -269,6 +269,25 @@ def test_parity_serpentine_maze(kengine, oracle, N, period):
     assert r.stats["passes"] > 4 * N // (r.stats["tile_w"] * 2)  # the maze inflates the passes
 
 
+@pytest.mark.parametrize("capfrac", ["0", "0.5", "0.9"])
+def test_list_fraction_cap_same_fixed_point(dymu, oracle, monkeypatch, capfrac):
+    """Kernel 5's per-pass target capped at a fraction of the active list
+    (DYMU_PRIO_CAPFRAC; 0.9 by default, 0 = off) changes the schedule, not the map:
+    the open grid and a serpentine maze (short lists, where the cap binds) both
+    match the oracle FMM."""
+    monkeypatch.setenv("DYMU_PRIO_CAPFRAC", capfrac)
+    N, g = 320, (160, 164)
+    F0 = oracle.synth_speed(N, N, seed=21, obst_frac=0.02, obst_seed=22, goal=g)
+    eng = dymu.Engine(kernel=5, prio_target=64)
+    try:
+        for F in (F0, serpentine_maze(F0, 32, 16)):
+            r = eng.solve(F, *g)
+            Tref, _ = oracle.fmm(F, g)
+            assert_parity(r.T, Tref)
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("mode", ["0", "1", "2"])
 @pytest.mark.parametrize("kernel", [3, 5])
 def test_convergence_check_modes(dymu, oracle, monkeypatch, mode, kernel):
