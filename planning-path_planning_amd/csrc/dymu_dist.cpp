@@ -407,12 +407,12 @@ class RcclTransport final : public Transport {
 struct BoardSlot {
   std::atomic<uint64_t> gen;       // generation of the published receive buffer
   std::atomic<uint64_t> cap;       // its elements per side
-  std::atomic<uint64_t> pre;       // (solve << 1) | ok
+  std::atomic<uint64_t> pre[2];    // (solve << 1) | ok, in slot solve % 2
   std::atomic<uint64_t> pushed;    // rounds whose push completed (running count)
   std::atomic<uint64_t> check[4];  // ((check + 1) << 32) | count, slot check % 4
   std::atomic<uint64_t> joined;    // 1 once the rank opened the board
   unsigned char handle[HIP_IPC_HANDLE_SIZE];
-  unsigned char pad[256 - 9 * 8 - HIP_IPC_HANDLE_SIZE];
+  unsigned char pad[256 - 10 * 8 - HIP_IPC_HANDLE_SIZE];
 };
 static_assert(sizeof(BoardSlot) == 256, "board slot");
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "board atomics");
@@ -482,17 +482,27 @@ class IpcTransport final : public Transport {
     return DYMU_OK;
   }
   int preflight(bool ok, hipStream_t, std::string* err) override {
+    // One slot per solve parity: a rank that leaves this pre-flight may post the next
+    // solve's before a slower peer has read this one's ok bit, and a single slot would
+    // hand that peer the NEXT solve's bit (a rejected slab read as accepted: the other
+    // ranks then entered the rounds of a solve the rejecting rank had abandoned).  A
+    // rank cannot get two solves ahead (the next pre-flight waits for every rank's post).
     const uint64_t s = ++solves;
-    board[rank].pre.store((s << 1) | (ok ? 1u : 0u), std::memory_order_release);
+    board[rank].pre[s & 1].store((s << 1) | (ok ? 1u : 0u), std::memory_order_release);
     bool all = true;
     for (int q = 0; q < world; ++q) {
-      if (!spin_until([&] { return (board[q].pre.load(std::memory_order_acquire) >> 1) >= s; })) {
+      uint64_t v = 0;
+      if (!spin_until([&] {
+            v = board[q].pre[s & 1].load(std::memory_order_acquire);
+            return (v >> 1) >= s;
+          })) {
+        const uint64_t seen = std::max(board[q].pre[0].load() >> 1, board[q].pre[1].load() >> 1);
         const std::string why = "timed out in the pre-flight of solve " + std::to_string(s) +
                                 " waiting for rank " + std::to_string(q) + " (at solve " +
-                                std::to_string(board[q].pre.load() >> 1) + "; a peer rank failed?)";
+                                std::to_string(seen) + "; a peer rank failed?)";
         return fail(err, "dymu_dist_solve", why.c_str(), DYMU_ERR_RCCL);
       }
-      all = all && (board[q].pre.load(std::memory_order_acquire) & 1u);
+      all = all && (v & 1u);
     }
     if (!all)
       return fail(err, "dymu_dist_solve", ok ? "another rank rejected its slab" : "invalid slab",
