@@ -62,8 +62,11 @@ def parse():
                          "shared-memory board (N ranks may share one GPU); 'python' = "
                          "dymu.sharded over torch.distributed")
     ap.add_argument("--passes-per-exchange", type=int, default=0,
-                    help="passes per exchange round (0: 4 for the native loop, 16 for the "
-                         "python loop; tools/vdist_rehearsal.py)")
+                    help="passes per exchange round (0: the native loop at N>1 times K = "
+                         "2/4/8 before the timed region and keeps the fastest, 4 at N=1; 16 for "
+                         "the python loop; tools/vdist_rehearsal.py)")
+    ap.add_argument("--no-k-tune", action="store_true",
+                    help="N>1 native loop: no K choice before the timed region (K = 4)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the row-slab path even at N=1 (exercises the RCCL code path)")
     ap.add_argument("--cpu-linear-size", type=int, default=2048,
@@ -452,6 +455,7 @@ def main():
                                "ipc": "hipIpc rows + shared-memory board, native C++ loop"}
                             .get(args.exchange, f"{args.backend}, torch.distributed loop") + ")"),
             "exchange_rounds_per_solve": tot.get("rounds", 0) / K,
+            "passes_per_exchange": tot.get("passes_per_exchange"),
             "passes_per_solve": tot["passes"] / K,
             # a tile is first relaxed one pass after its 4-neighbour that reaches it,
             # so no solve takes fewer passes than the largest Manhattan tile distance
@@ -468,6 +472,8 @@ def main():
         "roofline": roof,
         "cpu_baseline": None,
     }
+    if tot.get("k_autotune_ms"):  # untimed setup solves, one per candidate K (max over ranks)
+        line["config"]["k_autotune_ms"] = tot["k_autotune_ms"]
     if tot.get("variants"):
         line["variants"] = tot["variants"]
     if tot.get("parity") is not None:  # the sharded run's self-check (bench_sharded.self_check)

@@ -29,6 +29,9 @@ import dymu
 PROFILE_PERIOD = 64  # time every 64th pass launch of rank 0 (bench.py's roofline)
 
 
+K_CANDIDATES = (2, 4, 8)  # passes per exchange round tried before the timed region (N > 1)
+
+
 def _env_defaults():
     # `bench.py --sharded` without torchrun: a world of one
     os.environ.setdefault("RANK", "0")
@@ -89,8 +92,8 @@ def run(args):
         solver = ddist.DistSolver(eng, dev_idx, obj[0], rank, world, transport=transport)
         ranks_seen = solver.comm_count()  # what the transport itself sees
 
-        def solve():
-            return solver.solve(F.data_ptr(), T_buf.data_ptr(), N, N, N, g[0], g[1], K)
+        def solve(k=None):
+            return solver.solve(F.data_ptr(), T_buf.data_ptr(), N, N, N, g[0], g[1], k or K)
     else:
         from dymu.sharded import SlabSolver
 
@@ -98,7 +101,7 @@ def run(args):
                             passes_per_exchange=K, check_every=4)
         ranks_seen = dist.get_world_size()
 
-        def solve():
+        def solve(k=None):
             return solver.solve(F, T_buf, g[0], g[1])
     slabs = [None] * world
     dist.all_gather_object(slabs, [rank, row0, nrows])
@@ -107,6 +110,27 @@ def run(args):
                          f"{args.gpus}")
     for _ in range(args.warmup):
         solve()
+    k_tune = None
+    if native and world > 1 and not args.passes_per_exchange and not getattr(args, "no_k_tune", False):
+        # passes per exchange round, chosen on this node before the timed region: a round
+        # costs one P2P exchange (+ a 4-byte all-reduce every 4th), whose latency over
+        # xGMI the one-GPU rehearsal cannot see (K = 4 is best at <= 20 us
+        # per round, K = 6-8 above); every rank runs every candidate, the max over
+        # ranks of the best of two solves decides, and all ranks get the same K
+        k_tune = {}
+        for k in K_CANDIDATES:
+            best = float("inf")
+            for _ in range(2):
+                dist.barrier()
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                solve(k)
+                torch.cuda.synchronize()
+                el = torch.tensor([time.perf_counter() - t], dtype=torch.float64)
+                dist.all_reduce(el, op=dist.ReduceOp.MAX)
+                best = min(best, float(el.item()))
+            k_tune[k] = round(best * 1e3, 3)
+        K = min(k_tune, key=k_tune.get)  # identical on every rank (max-reduced times)
     prof = not args.no_profile and not fake
     if not fake:
         eng.set_profiling(PROFILE_PERIOD if prof else 0)
@@ -141,6 +165,9 @@ def run(args):
     tot["passes_sum_ranks"] = int(agg[2])
     tot["slab_cells"] = nrows * N  # rank 0's slab: the roofline's per-launch bytes
     tot["ranks_seen"] = ranks_seen
+    tot["passes_per_exchange"] = K
+    if k_tune is not None:
+        tot["k_autotune_ms"] = k_tune
     tot["slabs"] = sorted(slabs)
     if fake:
         _dump_fake(T_buf, row0, nrows, rank)

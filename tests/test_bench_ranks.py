@@ -89,6 +89,11 @@ def test_bench_gpus2_ipc_one_gpu_self_check():
     par = rec["parity"]
     assert par["ok"] and par["ghost_max_abs_diff"] == 0 and par["mismatched_cells"] == 0
     assert par["finite_cells"] == par["finite_cells_single"] > 0.9 * 2048 * 2048
+    # the passes-per-exchange choice made before the timed region: every candidate timed,
+    # the fastest kept (bench_sharded.K_CANDIDATES)
+    tune = rec["config"]["k_autotune_ms"]
+    assert sorted(int(k) for k in tune) == [2, 4, 8] and min(tune.values()) > 0
+    assert rec["config"]["passes_per_exchange"] == int(min(tune, key=tune.get))
 
 
 @pytest.mark.gpu
