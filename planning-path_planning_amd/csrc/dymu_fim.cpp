@@ -361,6 +361,11 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   // front re-relaxes the tiles downstream of it; DYMU_PRIO_CAPFRAC=0: off
   a.cap_frac = 0.9f;
   if (const char* kv = std::getenv("DYMU_PRIO_CAPFRAC")) a.cap_frac = (float)std::atof(kv);
+  // kernel 5: list entries carry their first-insertion key bin, so a key-deferred entry
+  // skips its tile loads (PassArgs::pack_bins); tile indices must fit below the bin field,
+  // and deterministic mode's histogram is rebuilt from the current keys instead
+  a.pack_bins = variant == 5 && D.ntiles <= kTileMask + 1u && !c->opts.deterministic;
+  if (const char* kv = std::getenv("DYMU_PACK_BINS")) a.pack_bins = a.pack_bins && std::atoi(kv);
   a.exact_sqrt = c->opts.exact_sqrt != 0;
   if (const char* kv = std::getenv("DYMU_EXACT_SQRT")) a.exact_sqrt = std::atoi(kv) != 0;
   if (c->opts.deterministic) {

@@ -93,7 +93,17 @@ struct PassArgs {
   // workgroup shard, summed (max / min for the radii) by the host
   uint32_t* pstat;
   int goal_tx, goal_ty;  // the goal's tile (radius = Manhattan tile distance from it)
+  // ---- kernel 5: list entries carry their first-insertion key bin (kPackShift) ----
+  // 1: this pass's enqueues write tile | (bin + 1) << kPackShift; an entry with a bin
+  // above the pass's threshold is then deferred on its CURRENT key before any tile
+  // load, one at or below it is relaxed without waiting on the key (the current key
+  // is never above the first-insertion one, so the decision is the key gate's)
+  int pack_bins;
 };
+// list entries: the tile index in the low kPackShift bits; bits above: 0 = no bin
+// (seeding kernels, merges), else the key bin + 1 the entry was first inserted with
+constexpr int kPackShift = 25;
+constexpr uint32_t kTileMask = (1u << kPackShift) - 1u;
 
 // per-pass statistics words (kernel 5)
 enum PassStat : int {

@@ -376,7 +376,7 @@ __global__ __launch_bounds__(256) void k_fim_pass_rb(PassArgs a) {
     uint32_t tile = 0;
     int tx = 0, ty = 0;
     if (has) {
-      tile = list_at(a.list_in, a.shard_cap, s_pref, li);
+      tile = list_at(a.list_in, a.shard_cap, s_pref, li) & kTileMask;
       tx = (int)(tile % (uint32_t)a.ntx);
       ty = (int)(tile / (uint32_t)a.ntx);
     }
@@ -956,13 +956,15 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_prio(PassArgs a) {
     atomicMin(&a.key_out[t], kb);
     atomicMin(&s_minout, kb);
     if (atomicMax(&a.tile_epoch[t], a.epoch) < a.epoch) {
-      atomicAdd(&s_hout[key_bin(bitsd(kb), origin_out, inv_delta)], 1u);
+      const int bin = key_bin(bitsd(kb), origin_out, inv_delta);
+      atomicAdd(&s_hout[bin], 1u);
+      const uint32_t ent = a.pack_bins ? (t | ((uint32_t)(bin + 1) << kPackShift)) : t;
       const uint32_t pos = atomicAdd(&s_nq, 1u);
       if (pos < QCAP) {
-        s_q[pos] = t;
+        s_q[pos] = ent;
       } else {
         const uint32_t gp = atomicAdd(&a.count_out[shard], 1u);
-        a.list_out[(uint64_t)shard * a.shard_cap + gp] = t;
+        a.list_out[(uint64_t)shard * a.shard_cap + gp] = ent;
       }
     }
   };
@@ -984,7 +986,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_prio(PassArgs a) {
     if (tid == 0) s_nwork = 0;
     __syncthreads();
     for (uint32_t e = s0 + tid; e < s1; e += blockDim.x) {
-      const uint32_t t = list_at(a.list_in, a.shard_cap, s_pref, e);
+      const uint32_t t = list_at(a.list_in, a.shard_cap, s_pref, e) & kTileMask;
       const unsigned long long kb = a.key_in[t];
       a.key_in[t] = kInfBits;
       if (key_bin(bitsd(kb), origin_in, inv_delta) <= bstar) {
@@ -1179,13 +1181,15 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     atomicMin(&a.key_out[t], kb);
     atomicMin(&s_minout, kb);
     if (atomicMax(&a.tile_epoch[t], a.epoch) < a.epoch) {
-      atomicAdd(&s_hout[key_bin(bitsd(kb), origin_out, inv_delta)], 1u);
+      const int bin = key_bin(bitsd(kb), origin_out, inv_delta);
+      atomicAdd(&s_hout[bin], 1u);
+      const uint32_t ent = a.pack_bins ? (t | ((uint32_t)(bin + 1) << kPackShift)) : t;
       const uint32_t pos = atomicAdd(&s_nq, 1u);
       if (pos < QCAP) {
-        s_q[pos] = t;
+        s_q[pos] = ent;
       } else {
         const uint32_t gp = atomicAdd(&a.count_out[shard], 1u);
-        a.list_out[(uint64_t)shard * a.shard_cap + gp] = t;
+        a.list_out[(uint64_t)shard * a.shard_cap + gp] = ent;
       }
     }
   };
@@ -1204,8 +1208,10 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     if (lane == 0) e = c0 + atomicAdd(&s_next, 1u);
     e = __builtin_amdgcn_readfirstlane(e);
     if (e >= c1) break;
-    const uint32_t tile =
+    const uint32_t ent =
         __builtin_amdgcn_readfirstlane(list_at_wave(a.list_in, a.shard_cap, s_pref, e, lane));
+    const uint32_t tile = ent & kTileMask;
+    const int pbin = (int)(ent >> kPackShift) - 1;  // first-insertion bin, -1: none
     const int tx = (int)(tile % (uint32_t)a.ntx);
     const int ty = (int)(tile / (uint32_t)a.ntx);
     if (a.checker && ((uint32_t)(tx + ty) + a.checker_parity) % 2u != 0u) {
@@ -1220,12 +1226,23 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       continue;
     }
     const unsigned long long kb = a.key_in[tile];
+    // a packed bin at or below b*: admitted (the current key is no higher); above: the
+    // current key decides now, before the tile loads a deferral would waste
+    if (pbin > bstar && key_bin(bitsd(kb), origin_in, inv_delta) > bstar) {
+      if (lane == 0) {
+        a.key_in[tile] = kInfBits;
+        enqueue(tile, kb);
+      }
+      ++my_defer;
+      continue;
+    }
+    const bool decided = pbin >= 0;
     if (lane < 4) ek[lane] = kInfBits;
     if (trace && tid == 0 && first) trace[6] = __builtin_amdgcn_s_memrealtime();
     bool capped = false;
     const int sweeps = visit16<APPROX>(
         a, img, ek, true, tx, ty, lane, capped,
-        [&] { return key_bin(bitsd(kb), origin_in, inv_delta) <= bstar; }, stop_at);
+        [&] { return decided || key_bin(bitsd(kb), origin_in, inv_delta) <= bstar; }, stop_at);
     if (lane == 0) a.key_in[tile] = kInfBits;
     if (sweeps < 0) {  // deferred to the next pass with its key
       if (lane == 0) enqueue(tile, kb);
@@ -1728,7 +1745,7 @@ __global__ __launch_bounds__(256) void k_rehist(const uint32_t* list, const uint
   const uint32_t n = counts[q];
   const double origin = *base, inv = 1.0 / *delta;
   for (uint32_t i = blockIdx.x * blockDim.x + tid; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t t = list[(uint64_t)q * cap + i];
+    const uint32_t t = list[(uint64_t)q * cap + i] & kTileMask;
     atomicAdd(&s_h[key_bin(bitsd(keys[t]), origin, inv)], 1u);
   }
   __syncthreads();

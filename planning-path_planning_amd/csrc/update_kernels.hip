@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void k_raise(RaiseArgs a) {
   for (uint32_t e = blockIdx.x * 4u + (uint32_t)wv; e < n; e += nw) {  // wave-uniform
     int k = 0;
     for (int s = 1; s < kShards; ++s) k += (e >= s_pref[s]) ? 1 : 0;
-    const uint32_t tile = a.list_in[(uint64_t)k * a.shard_cap + (e - s_pref[k])];
+    const uint32_t tile = a.list_in[(uint64_t)k * a.shard_cap + (e - s_pref[k])] & kTileMask;
     const int64_t i0 = (int64_t)(tile % a.ntx) * RT, j0 = (int64_t)(tile / a.ntx) * RT;
     auto at = [&](int64_t i, int64_t j) -> double {
       return (i >= 0 && j >= 0 && i < a.nx && j < a.ny) ? a.T[j * a.ld + i] : inf;
