@@ -6,6 +6,8 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT="$R/gpurun_out/pmc"
 mkdir -p "$OUT"
+# the calibration probe is git-ignored: build it here when this tree has none
+[ -x "$R/tools/pmc_calib" ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 "$R/tools/pmc_calib.hip" -o "$R/tools/pmc_calib" || exit 1
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/c1" -o run -- "$R/tools/pmc_calib" 16384 > "$OUT/c1.log" 2>&1 || exit 1
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/c2" -o run -- "$R/tools/pmc_calib" 16384 > "$OUT/c2.log" 2>&1 || exit 1
