@@ -288,6 +288,27 @@ def test_list_fraction_cap_same_fixed_point(dymu, oracle, monkeypatch, capfrac):
         eng.close()
 
 
+@pytest.mark.parametrize("pack", ["0", "1"])
+def test_packed_key_bins_same_fixed_point(dymu, oracle, monkeypatch, pack):
+    """Kernel 5's list entries with (DYMU_PACK_BINS=1, default) and without their
+    first-insertion key bin: the bin only moves the key gate before the tile loads, so
+    the open grid and a serpentine maze (many key-deferred entries, re-queued without a
+    bin by the capped visits) both reach the oracle's fixed point, with a small
+    per-pass target so that the threshold binds."""
+    monkeypatch.setenv("DYMU_PACK_BINS", pack)
+    N, g = 384, (100, 250)
+    F0 = oracle.synth_speed(N, N, seed=41, obst_frac=0.02, obst_seed=42, goal=g)
+    eng = dymu.Engine(kernel=5, prio_target=16)
+    try:
+        for F in (F0, serpentine_maze(F0, 48, 16)):
+            r = eng.solve(F, *g)
+            Tref, _ = oracle.fmm(F, g)
+            assert_parity(r.T, Tref)
+            assert r.stats["deferred"] > 0
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("mode", ["0", "1", "2"])
 @pytest.mark.parametrize("kernel", [3, 5])
 def test_convergence_check_modes(dymu, oracle, monkeypatch, mode, kernel):
