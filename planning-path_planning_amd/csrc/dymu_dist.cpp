@@ -87,6 +87,21 @@ int fail(std::string* err, const char* what, const char* detail, int code) {
   return code;
 }
 
+// the arguments every rank of one solve must agree on (a rank with another grid, goal
+// or K would run other rounds and leave its peers waiting), folded into 62 bits so that
+// its negation is an int64 too (the RCCL pre-flight reduces min(sig) and min(-sig))
+uint64_t call_signature(uint32_t nx, uint32_t ny, uint32_t gi, uint32_t gj, uint32_t K) {
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+  for (uint64_t v : {(uint64_t)nx, (uint64_t)ny, (uint64_t)gi, (uint64_t)gj, (uint64_t)K}) {
+    h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    h = (h ^ (h >> 30)) * 0xBF58476D1CE4E5B9ull;
+    h = (h ^ (h >> 27)) * 0x94D049BB133111EBull;
+  }
+  return (h ^ (h >> 31)) & ((1ull << 62) - 1);
+}
+
+constexpr const char* kSigMismatch = "the ranks passed different grids, goals or K";
+
 #define DHIP(err, expr)                                                                  \
   do {                                                                                   \
     hipError_t _e = (expr);                                                              \
@@ -203,8 +218,9 @@ class Transport {
   virtual ~Transport() = default;
   // receive rows and count words for an nx-wide grid (local; sets L[l].recv)
   virtual int alloc(std::vector<Local>& L, uint32_t nx, std::string* err) = 0;
-  // collective: every rank learns whether every rank can solve
-  virtual int preflight(bool ok, hipStream_t st, std::string* err) = 0;
+  // collective: every rank learns whether every rank can solve, and whether every
+  // rank passed the same solve signature (grid, goal, K: call_signature)
+  virtual int preflight(bool ok, uint64_t sig, hipStream_t st, std::string* err) = 0;
   // collective, after a successful pre-flight: peers' buffers mapped
   virtual int connect(std::string* err) {
     (void)err;
@@ -329,10 +345,14 @@ class RcclTransport final : public Transport {
   int32_t* d_cnt = nullptr;  // [2 parity][tot, sum], then the pre-flight flag
   uint64_t cap = 0;
   LoopRes pre;
+  int64_t* h_pre = nullptr;  // pre-flight (ok, sig, -sig): pinned host / device
+  int64_t* d_pre = nullptr;
 
   ~RcclTransport() override {
     if (comm) (void)ncclCommDestroy(comm);
     release();
+    if (h_pre) (void)hipHostFree(h_pre);
+    if (d_pre) (void)hipFree(d_pre);
   }
   void release() {
     if (rbuf) (void)hipFree(rbuf);
@@ -352,18 +372,23 @@ class RcclTransport final : public Transport {
     L[0].cap = cap;
     return DYMU_OK;
   }
-  int preflight(bool ok, hipStream_t st, std::string* err) override {
+  int preflight(bool ok, uint64_t sig, hipStream_t st, std::string* err) override {
+    if (!h_pre) DHIP(err, hipHostMalloc(&h_pre, sizeof(int64_t) * 3, hipHostMallocDefault));
+    if (!d_pre) DHIP(err, hipMalloc(&d_pre, sizeof(int64_t) * 3));
     DCALL(pre.init(err));
-    int32_t* flag = d_cnt + 4;
-    pre.h[2] = ok ? 1 : 0;
-    DHIP(err, hipMemcpyAsync(flag, pre.h + 2, sizeof(int32_t), hipMemcpyHostToDevice, st));
-    DNCCL(err, ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, comm, st));
-    DHIP(err, hipMemcpyAsync(pre.h + 2, flag, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    // min over ranks of (ok, sig, -sig): every rank ok, and min(sig) == max(sig)
+    h_pre[0] = ok ? 1 : 0;
+    h_pre[1] = (int64_t)sig;
+    h_pre[2] = -(int64_t)sig;
+    DHIP(err, hipMemcpyAsync(d_pre, h_pre, sizeof(int64_t) * 3, hipMemcpyHostToDevice, st));
+    DNCCL(err, ncclAllReduce(d_pre, d_pre, 3, ncclInt64, ncclMin, comm, st));
+    DHIP(err, hipMemcpyAsync(h_pre, d_pre, sizeof(int64_t) * 3, hipMemcpyDeviceToHost, st));
     DHIP(err, hipEventRecord(pre.ev[0], st));
     DCALL(wait_event(pre.ev[0], err));
-    if (pre.h[2] != 1)
+    if (h_pre[0] != 1)
       return fail(err, "dymu_dist_solve", ok ? "another rank rejected its slab" : "invalid slab",
                   DYMU_ERR_ARG);
+    if (h_pre[1] != -h_pre[2]) return fail(err, "dymu_dist_solve", kSigMismatch, DYMU_ERR_ARG);
     return DYMU_OK;
   }
   int32_t* tot(int, int par) override { return d_cnt + 2 * par; }
@@ -408,11 +433,12 @@ struct BoardSlot {
   std::atomic<uint64_t> gen;       // generation of the published receive buffer
   std::atomic<uint64_t> cap;       // its elements per side
   std::atomic<uint64_t> pre[2];    // (solve << 1) | ok, in slot solve % 2
+  std::atomic<uint64_t> sig[2];    // call_signature of that solve (stored before pre)
   std::atomic<uint64_t> pushed;    // rounds whose push completed (running count)
   std::atomic<uint64_t> check[4];  // ((check + 1) << 32) | count, slot check % 4
   std::atomic<uint64_t> joined;    // 1 once the rank opened the board
   unsigned char handle[HIP_IPC_HANDLE_SIZE];
-  unsigned char pad[256 - 10 * 8 - HIP_IPC_HANDLE_SIZE];
+  unsigned char pad[256 - 12 * 8 - HIP_IPC_HANDLE_SIZE];
 };
 static_assert(sizeof(BoardSlot) == 256, "board slot");
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "board atomics");
@@ -481,15 +507,16 @@ class IpcTransport final : public Transport {
     L[0].cap = cap;
     return DYMU_OK;
   }
-  int preflight(bool ok, hipStream_t, std::string* err) override {
+  int preflight(bool ok, uint64_t sig, hipStream_t, std::string* err) override {
     // One slot per solve parity: a rank that leaves this pre-flight may post the next
     // solve's before a slower peer has read this one's ok bit, and a single slot would
     // hand that peer the NEXT solve's bit (a rejected slab read as accepted: the other
     // ranks then entered the rounds of a solve the rejecting rank had abandoned).  A
     // rank cannot get two solves ahead (the next pre-flight waits for every rank's post).
     const uint64_t s = ++solves;
+    board[rank].sig[s & 1].store(sig, std::memory_order_relaxed);
     board[rank].pre[s & 1].store((s << 1) | (ok ? 1u : 0u), std::memory_order_release);
-    bool all = true;
+    bool all = true, same = true;
     for (int q = 0; q < world; ++q) {
       uint64_t v = 0;
       if (!spin_until([&] {
@@ -503,10 +530,12 @@ class IpcTransport final : public Transport {
         return fail(err, "dymu_dist_solve", why.c_str(), DYMU_ERR_RCCL);
       }
       all = all && (v & 1u);
+      same = same && board[q].sig[s & 1].load(std::memory_order_relaxed) == sig;
     }
     if (!all)
       return fail(err, "dymu_dist_solve", ok ? "another rank rejected its slab" : "invalid slab",
                   DYMU_ERR_ARG);
+    if (!same) return fail(err, "dymu_dist_solve", kSigMismatch, DYMU_ERR_ARG);
     return DYMU_OK;
   }
   int connect(std::string* err) override {
@@ -619,7 +648,7 @@ class VirtualTransport final : public Transport {
     DHIP(err, hipMalloc(&sum, sizeof(int32_t) * 2));
     return DYMU_OK;
   }
-  int preflight(bool ok, hipStream_t, std::string* err) override {
+  int preflight(bool ok, uint64_t, hipStream_t, std::string* err) override {
     return ok ? DYMU_OK : fail(err, "dymu_vdist_solve", "invalid slab", DYMU_ERR_ARG);
   }
   int32_t* tot(int l, int par) override {
@@ -792,7 +821,7 @@ int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t 
                               DYMU_ERR_NOMEM));
   const bool ok = nx > 0 && ny > 0 && goal_i < nx && goal_j < ny &&
                   make_slab(F_slab, T_buf, ld, nx, ny, goal_j, d->rank, d->world, &L[0].s) == DYMU_OK;
-  int rc = d->xp->preflight(ok, st, err);
+  int rc = d->xp->preflight(ok, call_signature(nx, ny, goal_i, goal_j, K), st, err);
   if (rc) return rc == DYMU_ERR_ARG ? rc : abort_dist(d, rc);
   rc = d->xp->connect(err);
   if (rc) return abort_dist(d, rc);
@@ -828,7 +857,7 @@ int dymu_vdist_solve(dymu_ctx* const* ctxs, int world, const double* const* F_sl
   LoopRes R;
   std::string err;
   DCALL(X.alloc(L, nx, &err));
-  DCALL(X.preflight(true, st, &err));
+  DCALL(X.preflight(true, call_signature(nx, ny, goal_i, goal_j, K), st, &err));
   for (int r = 0; r < world; ++r)
     DCALL(dymu_dom_begin(ctxs[r], &L[r].s.dom, L[r].s.goal_local >= 0 ? goal_i : 0,
                          L[r].s.goal_local, stream));

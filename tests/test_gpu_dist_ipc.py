@@ -14,7 +14,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank):
+def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank, bad_kind):
     os.environ.setdefault("DYMU_DIST_TIMEOUT_S", "90")
     import sys
     import time
@@ -35,9 +35,11 @@ def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank):
         dT = eng.alloc(8 * (nrows + 2) * nx)
         eng.h2d(dF, np.ascontiguousarray(F_full[row0:row0 + nrows]))
         pre = None
-        if bad_rank is not None:  # one rank passes an invalid slab: all ranks must refuse
+        if bad_rank is not None:  # one rank passes an invalid slab / another K: all refuse
+            bad = rank == bad_rank
             try:
-                solver.solve(0 if rank == bad_rank else dF, dT, nx, nx, ny, goal[0], goal[1], 4)
+                solver.solve(0 if bad and bad_kind == "slab" else dF, dT, nx, nx, ny, goal[0],
+                             goal[1], 3 if bad and bad_kind == "k" else 4)
                 pre = "solved"
             except dymu.DymuError as e:
                 pre = e.status
@@ -55,7 +57,7 @@ def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank):
         out_q.put((rank, 0, None, None, 0, None, f"rank {rank}: {e!r} {marks}"))
 
 
-def _run(oracle, world, nx, ny, goal, engine_kw, bad_rank=None):
+def _run(oracle, world, nx, ny, goal, engine_kw, bad_rank=None, bad_kind="slab"):
     import multiprocessing as mp
     from dymu import dist
 
@@ -64,7 +66,7 @@ def _run(oracle, world, nx, ny, goal, engine_kw, bad_rank=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker,
-                         args=(r, world, uid, nx, ny, goal, F, q, engine_kw, bad_rank))
+                         args=(r, world, uid, nx, ny, goal, F, q, engine_kw, bad_rank, bad_kind))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -97,7 +99,11 @@ def test_ipc_loop_across_processes_matches_oracle(dymu, oracle, world, nx, ny, g
     _run(oracle, world, nx, ny, goal, engine_kw)
 
 
-def test_ipc_preflight_rejects_on_every_rank(dymu, oracle):
-    """A rank-local argument error (a null speed slab on rank 1) fails every rank
-    with DYMU_ERR_ARG through the collective pre-flight; the next solve works."""
-    _run(oracle, 3, 160, 200, (80, 100), dict(kernel=5, prio_target=8), bad_rank=1)
+@pytest.mark.parametrize("bad_kind", ["slab", "k"])
+def test_ipc_preflight_rejects_on_every_rank(dymu, oracle, bad_kind):
+    """A rank-local argument error (a null speed slab on rank 1) or a rank passing
+    another K than its peers (which would run other rounds and leave them waiting)
+    fails every rank with DYMU_ERR_ARG through the collective pre-flight; the next
+    solve works."""
+    _run(oracle, 3, 160, 200, (80, 100), dict(kernel=5, prio_target=8), bad_rank=1,
+         bad_kind=bad_kind)
