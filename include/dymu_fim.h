@@ -61,11 +61,12 @@ typedef struct dymu_opts {
                            passes on 16x16 tiles */
   int prio_target;      /* kernels 4/5: tiles relaxed per pass; 0 = default
                            (64 per CU for 4, 8 per CU for 5) */
-  int exact_sqrt;       /* kernel 5: 1 = correctly rounded sqrt in the sweeps (every update
-                           bit-identical to the reference formula); 0 = default: one
-                           Goldschmidt step folded into the candidate, <= 36 ulp of the
-                           reference candidate, solve error vs the reference FMM unchanged
-                           (<= 6e-15 rel) */
+  int exact_sqrt;       /* kernel 5: 1 = correctly rounded sqrt in the sweeps; 0 = default:
+                           one Goldschmidt step folded into the candidate.  Both use the
+                           monotone combine min(Tx,Ty) + h (one rounding at the scale of T,
+                           within 1 ulp of the reference candidate plus the sqrt's error),
+                           so the FIM's min over history does not accumulate a rounding
+                           bias along long paths (DESIGN.md s3, s4 "Monotone combine") */
   int deterministic;    /* 1 = bit-reproducible maps: kernel 5 with checkerboard passes (a
                            pass relaxes tiles of one colour only, so no tile reads a halo
                            another wave is writing) and no sweep deadline; ~2x the passes.
@@ -208,8 +209,11 @@ int dymu_synth_speed(dymu_ctx* ctx, double* dF, uint32_t nx, uint32_t ny, uint64
 
 /* Arithmetic self-test: out[k] = the kernels' Eikonal candidate for
  * (Tx[k], Ty[k], C[k]) (reference :531-535), computed by the same device code
- * the pass kernels use (fast = 1: the range-restricted correctly rounded sqrt;
- * fast = 2: kernel 5's default sweep sqrt, one Goldschmidt step).
+ * the pass kernels use (fast = 1: the range-restricted correctly rounded sqrt in
+ * the reference's combine, kernels 3/4; fast = 2: kernel 5's default sweep
+ * candidate, monotone combine + one Goldschmidt step; fast = 3: kernel 5 with
+ * exact_sqrt, monotone combine + correctly rounded sqrt; fast = 4: the v31 sweep
+ * candidate, kept for A/B).
  * Device pointers; blocks until done. */
 int dymu_eikonal_batch(dymu_ctx* ctx, const double* tx, const double* ty, const double* c,
                        double* out, uint64_t n, int fast);

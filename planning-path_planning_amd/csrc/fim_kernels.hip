@@ -208,22 +208,47 @@ __device__ __forceinline__ double two_sided_approx(double ty, double d, double c
   return __builtin_fma(s, t, __builtin_fma(d, 0.5, ty));
 }
 
-// two_sided_approx on two independent cells, statement by statement interleaved
-// (same operations, bit-identical)
-__device__ __forceinline__ void two_sided_approx2(double ty0, double d0, double c0, double ty1,
-                                                  double d1, double c1, double& v0, double& v1) {
+// The monotone combine (v32, kernel 5's sweeps).  The reference rounds the
+// two-sided candidate twice at the scale of T -- RN(RN(Tx + Ty) + sqrt) / 2 --
+// so a larger input can round to a smaller candidate by an ulp of T.  The FIM
+// evaluates a cell many times while its inputs converge from above and keeps
+// the minimum (:537), i.e. the luckiest of those roundings: a downward bias of
+// ~0.002 ulp per cell that adds up along a path (1.21e-12 on the 16384^2
+// serpentine maze's ~4 M-cell corridors).  Written as
+//   T' = min(Tx,Ty) + h,  h = (|Tx - Ty| + sqrt(2C^2 - d^2)) / 2  (two-sided)
+//                         h = C                                  (one-sided)
+// the candidate is rounded ONCE at the scale of T, the correction h carries
+// only errors at the scale of C, and the candidate is monotone in (Tx, Ty)
+// up to those C-scale errors: the min over history is then the last
+// evaluation's value, and the map is the fixed point of the update rather
+// than its luckiest rounding (tools/mono_sim.c: the bias no longer grows with
+// the path length).  The one-sided value m + C is the reference's, bit for bit.
+// h of the approximate sweep sqrt: y0 = rsq(r), s = r*y0,
+// sqrt(r)/2 ~ s*(0.75 - (y0/4)*s), so h = fma(s, t, |d|/2)
+__device__ __forceinline__ double half_two_sided_approx(double d, double c2x2) {
+  const double r = __builtin_fma(-d, d, c2x2);
+  const double y0 = __builtin_amdgcn_rsq(r);
+  const double s = r * y0;
+  const double t = __builtin_fma(-(y0 * 0.25), s, 0.75);
+  return __builtin_fma(s, t, fabs(d) * 0.5);
+}
+
+// half_two_sided_approx on two independent cells, statement by statement
+// interleaved (same operations, bit-identical)
+__device__ __forceinline__ void half_two_sided_approx2(double d0, double c0, double d1, double c1,
+                                                       double& h0, double& h1) {
   const double r0 = __builtin_fma(-d0, d0, c0);
   const double r1 = __builtin_fma(-d1, d1, c1);
   const double y0 = __builtin_amdgcn_rsq(r0);
   const double y1 = __builtin_amdgcn_rsq(r1);
-  const double h0 = __builtin_fma(d0, 0.5, ty0);
-  const double h1 = __builtin_fma(d1, 0.5, ty1);
+  const double a0 = fabs(d0) * 0.5;
+  const double a1 = fabs(d1) * 0.5;
   const double s0 = r0 * y0;
   const double s1 = r1 * y1;
   const double t0 = __builtin_fma(-(y0 * 0.25), s0, 0.75);
   const double t1 = __builtin_fma(-(y1 * 0.25), s1, 0.75);
-  v0 = __builtin_fma(s0, t0, h0);
-  v1 = __builtin_fma(s1, t1, h1);
+  h0 = __builtin_fma(s0, t0, a0);
+  h1 = __builtin_fma(s1, t1, a1);
 }
 
 // One cell of the reference update (:504-537) against the image.  Preconditions
@@ -259,7 +284,10 @@ __device__ __forceinline__ bool rb_update(double* img, int slot, double f, doubl
 
 // The update of rb_update without the skip test, for the arithmetic self-test
 // (dymu_eikonal_batch): candidate T' from (Tx, Ty, C) as at :531-535.
-// MODE 0: sqrt(), 1: sqrt_cr_fast (bit-identical), 2: the approximate sweep sqrt
+// MODE 0: sqrt(), 1: sqrt_cr_fast (bit-identical), 2: kernel 5's default sweep
+// candidate (monotone combine, approximate sqrt), 3: kernel 5's exact_sqrt sweep
+// candidate (monotone combine, correctly rounded sqrt), 4: v31's sweep candidate
+// (two_sided_approx, kept for the A/B of the combine)
 template <int MODE>
 __device__ __forceinline__ double update_value(double tx_, double ty_, double f) {
   const double m = minnn(tx_, ty_);
@@ -267,7 +295,9 @@ __device__ __forceinline__ double update_value(double tx_, double ty_, double f)
   const double dd = tx_ - ty_;
   if (fabs(dd) < f) {
     const double r = 2.0 * (f * f) - dd * dd;
-    if (MODE == 2) return two_sided_approx(ty_, dd, 2.0 * (f * f));
+    if (MODE == 2) return m + half_two_sided_approx(dd, 2.0 * (f * f));
+    if (MODE == 3) return m + (fabs(dd) + sqrt_cr_fast(__builtin_fma(-dd, dd, 2.0 * (f * f)))) * 0.5;
+    if (MODE == 4) return two_sided_approx(ty_, dd, 2.0 * (f * f));
     const double sq = MODE == 1 ? sqrt_cr_fast(r) : sqrt(r);
     return ((tx_ + ty_) + sq) * 0.5;
   }
@@ -653,12 +683,14 @@ __device__ __forceinline__ void rb_update2(const double* p, const double* pn, co
   const double m0 = vmin64(tx0, ty0), m1 = vmin64(tx1, ty1);
   {
     const double d0 = tx0 - ty0, d1 = tx1 - ty1;
-    double v0, v1;  // two-sided candidates
+    // the monotone combine (half_two_sided_approx): T' = min + h, h = C on the
+    // one-sided branch; the select comes before the one add at the scale of T
+    double h0, h1;  // two-sided half-sums (|d| + sqrt(2C^2 - d^2)) / 2
     if constexpr (FAST && APPROX) {
       // an obstacle (f = inf) gives NaN here (rsq(inf) * inf), which v_min ignores
-      two_sided_approx2(ty0, d0, c20, ty1, d1, c21, v0, v1);
+      half_two_sided_approx2(d0, c20, d1, c21, h0, h1);
     } else {
-      const double r0 = c20 - d0 * d0, r1 = c21 - d1 * d1;
+      const double r0 = __builtin_fma(-d0, d0, c20), r1 = __builtin_fma(-d1, d1, c21);
       double q0, q1;
       if constexpr (FAST) {
         sqrt_cr_fast2<APPROX>(r0, r1, q0, q1);
@@ -666,11 +698,11 @@ __device__ __forceinline__ void rb_update2(const double* p, const double* pn, co
         q0 = sqrt(r0);
         q1 = sqrt(r1);
       }
-      v0 = ((tx0 + ty0) + q0) * 0.5;
-      v1 = ((tx1 + ty1) + q1) * 0.5;
+      h0 = (fabs(d0) + q0) * 0.5;
+      h1 = (fabs(d1) + q1) * 0.5;
     }
-    const double u0 = fabs(d0) < f0 ? v0 : m0 + f0;
-    const double u1 = fabs(d1) < f1 ? v1 : m1 + f1;
+    const double u0 = m0 + (fabs(d0) < f0 ? h0 : f0);
+    const double u1 = m1 + (fabs(d1) < f1 ? h1 : f1);
     ch0 = u0 < t0;
     ch1 = u1 < t1;
     // min(t, u) == (u < t ? u : t): one v_min_f64 on the chain to the LDS write
@@ -1690,6 +1722,12 @@ hipError_t launch_eikonal_batch(const double* tx, const double* ty, const double
   if (blocks == 0) return hipSuccess;
   if (fast == 2)
     hipLaunchKernelGGL(k_eikonal_batch<2>, dim3((unsigned)blocks), dim3(256), 0, st, tx, ty, c,
+                       out, n);
+  else if (fast == 3)
+    hipLaunchKernelGGL(k_eikonal_batch<3>, dim3((unsigned)blocks), dim3(256), 0, st, tx, ty, c,
+                       out, n);
+  else if (fast == 4)
+    hipLaunchKernelGGL(k_eikonal_batch<4>, dim3((unsigned)blocks), dim3(256), 0, st, tx, ty, c,
                        out, n);
   else if (fast)
     hipLaunchKernelGGL(k_eikonal_batch<1>, dim3((unsigned)blocks), dim3(256), 0, st, tx, ty, c,

@@ -346,8 +346,10 @@ class Engine:
     def eikonal_batch(self, tx: np.ndarray, ty: np.ndarray, c: np.ndarray,
                       fast=True) -> np.ndarray:
         """The kernels' update arithmetic on the GPU (bit-level self-test).
-        fast: False = sqrt(), True = the correctly rounded sweep sqrt, 2 = the
-        approximate sweep sqrt of kernel 5 (dymu_opts.exact_sqrt = 0)."""
+        fast: False = sqrt(), True = the correctly rounded sqrt in the reference's
+        combine (kernels 3/4), 2 = kernel 5's default sweep candidate (monotone
+        combine, approximate sqrt), 3 = kernel 5's exact_sqrt sweep candidate
+        (monotone combine, correctly rounded sqrt), 4 = v31's sweep candidate."""
         arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (tx, ty, c)]
         n = arrs[0].size
         ptrs = [self.alloc(8 * n) for _ in range(4)]
@@ -355,7 +357,7 @@ class Engine:
             for p, a in zip(ptrs, arrs):
                 self.h2d(p, a)
             _check(self._lib.dymu_eikonal_batch(self.ctx, ptrs[0], ptrs[1], ptrs[2], ptrs[3], n,
-                                                2 if fast == 2 else 1 if fast else 0),
+                                                fast if fast in (2, 3, 4) else 1 if fast else 0),
                    self.ctx)
             out = np.empty(n)
             self.d2h(out, ptrs[3])

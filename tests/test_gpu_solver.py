@@ -189,12 +189,15 @@ def test_update_arithmetic_bit_exact(engine, oracle, fast):
     assert np.array_equal(out, r)
 
 
-def test_update_arithmetic_approx_sqrt(engine):
-    """Kernel 5's default two-sided candidate (dymu_opts.exact_sqrt = 0: one
-    Goldschmidt step after v_rsq_f64, folded into the combine; two_sided_approx)
-    is within 36 ulp of the reference formula's candidate (tools/sqrt_probe.hip:
-    805 M operands with Tx, Ty >= 0, max 36 ulp, 0.66% not correctly rounded),
-    i.e. <= 1e-14 relative; the one-sided and infinite cases are bit-identical."""
+@pytest.mark.parametrize("fast", [2, 3, 4])
+def test_update_arithmetic_approx_sqrt(engine, fast):
+    """Kernel 5's sweep candidates: 2 = the default (monotone combine min + h,
+    one Goldschmidt step after v_rsq_f64), 3 = exact_sqrt (monotone combine,
+    correctly rounded sqrt), 4 = v31's combine (two_sided_approx).  Each is within
+    40 ulp of the reference formula's candidate (the sqrt term within 36 ulp,
+    tools/sqrt_probe.hip; the monotone combine rounds once where the reference
+    rounds twice, <= 1 ulp apart), i.e. <= 1e-14 relative; with the correctly
+    rounded sqrt within 2 ulp.  The one-sided and infinite cases are bit-identical."""
     rng = np.random.default_rng(11)
     n = 1 << 21
     c = np.exp(rng.uniform(np.log(1e-3), np.log(1e3), n))
@@ -202,15 +205,39 @@ def test_update_arithmetic_approx_sqrt(engine):
     ty = np.abs(tx + rng.normal(0, 1, n) * c)
     tx[::97] = np.inf
     ty[::89] = np.inf
-    out = engine.eikonal_batch(tx, ty, c, fast=2)
+    out = engine.eikonal_batch(tx, ty, c, fast=fast)
     with np.errstate(invalid="ignore"):
         d = tx - ty
         two = (np.abs(d) < c) & np.isfinite(tx) & np.isfinite(ty)
         q = np.sqrt(2 * (c * c) - d * d)
         r = np.where(two, (tx + ty + q) / 2, np.minimum(tx, ty) + c)
     assert np.array_equal(out[~two], r[~two])
-    assert np.all(np.abs(out[two] - r[two]) <= 40 * np.spacing(r[two]))
+    ulps = 2 if fast == 3 else 40
+    assert np.all(np.abs(out[two] - r[two]) <= ulps * np.spacing(r[two]))
     assert np.max(np.abs(out[two] - r[two]) / r[two]) <= 1e-14
+
+
+def test_update_monotone_combine(engine):
+    """The monotone combine (DESIGN.md s4 "Monotone combine"): raising Tx or Ty by
+    one ulp almost never lowers the candidate, where the reference's two roundings
+    at the scale of T -- RN(RN(Tx + Ty) + sqrt) / 2 -- lower it in a few percent of
+    the two-sided cases.  That non-monotonicity is what the FIM's min over history
+    turns into a bias along long paths (the 16384^2 maze, tests/test_gpu_maze.py)."""
+    rng = np.random.default_rng(5)
+    n = 1 << 20
+    c = np.exp(rng.uniform(np.log(1e-1), np.log(1e1), n))
+    tx = rng.uniform(0, 1e4, n)
+    ty = np.abs(tx + rng.normal(0, 0.5, n) * c)
+    two = np.abs(tx - ty) < c
+    rate = {}
+    for fast in (True, 4, 2, 3):
+        a = engine.eikonal_batch(tx, ty, c, fast=fast)
+        bx = engine.eikonal_batch(np.nextafter(tx, np.inf), ty, c, fast=fast)
+        by = engine.eikonal_batch(tx, np.nextafter(ty, np.inf), c, fast=fast)
+        rate[fast] = float(((bx < a) | (by < a))[two].mean())
+    assert rate[True] > 0.01  # the reference arithmetic (kernels 3/4)
+    assert rate[3] <= 1e-4, rate
+    assert rate[2] <= rate[True] / 10, rate
 
 
 def test_exact_sqrt_option(dymu, oracle):
