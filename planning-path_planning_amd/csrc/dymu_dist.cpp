@@ -29,7 +29,12 @@
 // sender's state after round m: RCCL orders the receive after the send on both
 // streams, the virtual copies are on the one stream, and the IPC push is
 // host-synchronised per round (exchange() returns once this rank's push of
-// round m completed and both neighbours have reported theirs).
+// round m completed and both neighbours have reported theirs).  The IPC receive
+// rows are double-buffered by round parity, so a push never lands in the rows
+// the neighbour's current round is merging: round m's push fills parity m % 2,
+// round m+1's merge reads it, and the push of round m+2 into the same parity
+// starts only after the neighbour reported round m+1's push -- after its round
+// m+1 passes, merge included, completed.
 // Kernel 3/4 slabs (no fused round) keep the v1 round: dymu_dom_run, the
 // transfer, then one dymu_dom_exchange launch that merges and counts.
 //
@@ -437,8 +442,9 @@ struct BoardSlot {
   std::atomic<uint64_t> pushed;    // rounds whose push completed (running count)
   std::atomic<uint64_t> check[4];  // ((check + 1) << 32) | count, slot check % 4
   std::atomic<uint64_t> joined;    // 1 once the rank opened the board
+  std::atomic<uint64_t> aborted;   // 1 once the rank gave up the collective sequence
   unsigned char handle[HIP_IPC_HANDLE_SIZE];
-  unsigned char pad[256 - 12 * 8 - HIP_IPC_HANDLE_SIZE];
+  unsigned char pad[256 - 13 * 8 - HIP_IPC_HANDLE_SIZE];
 };
 static_assert(sizeof(BoardSlot) == 256, "board slot");
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "board atomics");
@@ -450,7 +456,7 @@ class IpcTransport final : public Transport {
   bool owner = false;
   BoardSlot* board = nullptr;
   size_t board_bytes = 0;
-  double* recv = nullptr;  // [2 side][cap], exported
+  double* recv = nullptr;  // [2 parity][2 side][cap], exported
   uint64_t cap = 0;
   uint64_t gen = 0;        // generation of recv
   int32_t* d_cnt = nullptr;  // [2 parity] local counts
@@ -458,6 +464,29 @@ class IpcTransport final : public Transport {
   uint64_t peer_gen[2] = {0, 0}, peer_cap[2] = {0, 0};
   uint64_t solves = 0, rounds = 0, checks = 0;
   hipEvent_t ev = nullptr;
+
+  // spin_until that also gives up as soon as any rank has aborted (its abort() after
+  // an error): the peers fail at once instead of after the full timeout
+  bool peer_aborted() const {
+    for (int q = 0; q < world; ++q)
+      if (board[q].aborted.load(std::memory_order_acquire)) return true;
+    return false;
+  }
+  template <class Cond>
+  int wait(Cond&& cond, const char* what, std::string* err) {
+    bool gone = false;
+    const bool ok = spin_until([&] {
+      if (cond()) return true;
+      gone = peer_aborted();
+      return gone;
+    });
+    if (gone) return fail(err, "dymu_dist_solve", "a peer rank aborted the solve", DYMU_ERR_RCCL);
+    if (!ok) return fail(err, "dymu_dist_solve", what, DYMU_ERR_RCCL);
+    return DYMU_OK;
+  }
+  void abort() override {
+    if (board) board[rank].aborted.store(1, std::memory_order_release);
+  }
 
   ~IpcTransport() override {
     for (auto& p : peer)
@@ -499,11 +528,11 @@ class IpcTransport final : public Transport {
       if (recv) DHIP(err, hipFree(recv));
       recv = nullptr;
       cap = 0;
-      DHIP(err, hipMalloc(&recv, sizeof(double) * 2 * (uint64_t)nx));
+      DHIP(err, hipMalloc(&recv, sizeof(double) * 4 * (uint64_t)nx));
       cap = nx;
       ++gen;
     }
-    L[0].recv = recv;
+    L[0].recv = recv + (rounds & 1) * 2 * cap;  // the parity the next merge reads
     L[0].cap = cap;
     return DYMU_OK;
   }
@@ -519,16 +548,14 @@ class IpcTransport final : public Transport {
     bool all = true, same = true;
     for (int q = 0; q < world; ++q) {
       uint64_t v = 0;
-      if (!spin_until([&] {
-            v = board[q].pre[s & 1].load(std::memory_order_acquire);
-            return (v >> 1) >= s;
-          })) {
-        const uint64_t seen = std::max(board[q].pre[0].load() >> 1, board[q].pre[1].load() >> 1);
-        const std::string why = "timed out in the pre-flight of solve " + std::to_string(s) +
-                                " waiting for rank " + std::to_string(q) + " (at solve " +
-                                std::to_string(seen) + "; a peer rank failed?)";
-        return fail(err, "dymu_dist_solve", why.c_str(), DYMU_ERR_RCCL);
-      }
+      const uint64_t seen0 = std::max(board[q].pre[0].load() >> 1, board[q].pre[1].load() >> 1);
+      const std::string why = "timed out in the pre-flight of solve " + std::to_string(s) +
+                              " waiting for rank " + std::to_string(q) + " (at solve " +
+                              std::to_string(seen0) + "; a peer rank failed?)";
+      DCALL(wait([&] {
+              v = board[q].pre[s & 1].load(std::memory_order_acquire);
+              return (v >> 1) >= s;
+            }, why.c_str(), err));
       all = all && (v & 1u);
       same = same && board[q].sig[s & 1].load(std::memory_order_relaxed) == sig;
     }
@@ -549,10 +576,10 @@ class IpcTransport final : public Transport {
     for (int side = 0; side < 2; ++side) {
       const int q = side == 0 ? rank - 1 : rank + 1;
       if (q < 0 || q >= world) continue;
-      // every rank allocates at the same solves (same nx sequence): same generation
-      if (!spin_until([&] { return board[q].gen.load(std::memory_order_acquire) >= gen; }))
-        return fail(err, "dymu_dist_solve", "timed out waiting for a peer's receive rows",
-                    DYMU_ERR_RCCL);
+      // every rank allocates after the same accepted pre-flights (the signature pins nx):
+      // the same generation
+      DCALL(wait([&] { return board[q].gen.load(std::memory_order_acquire) >= gen; },
+                 "timed out waiting for a peer's receive rows", err));
       const uint64_t g = board[q].gen.load(std::memory_order_acquire);
       if (g == peer_gen[side] && peer[side]) continue;
       if (peer[side]) DHIP(err, hipIpcCloseMemHandle(peer[side]));
@@ -570,16 +597,19 @@ class IpcTransport final : public Transport {
   int32_t* tot(int, int par) override { return d_cnt + par; }
   const int32_t* post_src(int par) override { return d_cnt + par; }
   int exchange(std::vector<Local>& L, uint32_t nx, hipStream_t st, std::string* err) override {
-    const Local& l = L[0];
+    Local& l = L[0];
     // push: my first row into rank-1's "from rank+1" row, my last into rank+1's
-    // "from rank-1" row (ordered after this round's passes on my stream)
+    // "from rank-1" row (ordered after this round's passes on my stream), both in
+    // the receive parity of this round
+    const uint64_t par = rounds & 1;
     if (l.s.lo)
-      DHIP(err, hipMemcpyAsync(peer[0] + peer_cap[0], l.s.row(0), sizeof(double) * nx,
-                               hipMemcpyDeviceToDevice, st));
+      DHIP(err, hipMemcpyAsync(peer[0] + (2 * par + 1) * peer_cap[0], l.s.row(0),
+                               sizeof(double) * nx, hipMemcpyDeviceToDevice, st));
     if (l.s.hi)
-      DHIP(err, hipMemcpyAsync(peer[1], l.s.row(1), sizeof(double) * nx, hipMemcpyDeviceToDevice,
-                               st));
+      DHIP(err, hipMemcpyAsync(peer[1] + 2 * par * peer_cap[1], l.s.row(1), sizeof(double) * nx,
+                               hipMemcpyDeviceToDevice, st));
     const uint64_t m = ++rounds;
+    l.recv = recv + par * 2 * cap;  // the next round merges what the neighbours pushed now
     if (!l.s.lo && !l.s.hi) return DYMU_OK;
     DHIP(err, hipEventRecord(ev, st));
     DCALL(wait_event(ev, err));
@@ -587,9 +617,8 @@ class IpcTransport final : public Transport {
     for (int side = 0; side < 2; ++side) {
       const int q = side == 0 ? rank - 1 : rank + 1;
       if ((side == 0 && !l.s.lo) || (side == 1 && !l.s.hi)) continue;
-      if (!spin_until([&] { return board[q].pushed.load(std::memory_order_acquire) >= m; }))
-        return fail(err, "dymu_dist_solve", "timed out waiting for a neighbour's rows",
-                    DYMU_ERR_RCCL);
+      DCALL(wait([&] { return board[q].pushed.load(std::memory_order_acquire) >= m; },
+                 "timed out waiting for a neighbour's rows", err));
     }
     return DYMU_OK;
   }
@@ -601,11 +630,10 @@ class IpcTransport final : public Transport {
     int64_t g = 0;
     for (int q = 0; q < world; ++q) {
       uint64_t v = 0;
-      if (!spin_until([&] {
-            v = board[q].check[c % 4].load(std::memory_order_acquire);
-            return (v >> 32) >= c + 1;
-          }))
-        return fail(err, "dymu_dist_solve", "timed out in the count reduction", DYMU_ERR_RCCL);
+      DCALL(wait([&] {
+              v = board[q].check[c % 4].load(std::memory_order_acquire);
+              return (v >> 32) >= c + 1;
+            }, "timed out in the count reduction", err));
       g += (int64_t)(uint32_t)v;
     }
     *global = g;
@@ -816,13 +844,16 @@ int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t 
   std::vector<Local> L(1);
   L[0].ctx = d->ctx;
   L[0].rank = d->rank;
-  if (d->xp->alloc(L, nx ? nx : 1, err) != DYMU_OK)
-    return abort_dist(d, fail(err, "dymu_dist_solve", "receive rows: out of memory",
-                              DYMU_ERR_NOMEM));
   const bool ok = nx > 0 && ny > 0 && goal_i < nx && goal_j < ny &&
                   make_slab(F_slab, T_buf, ld, nx, ny, goal_j, d->rank, d->world, &L[0].s) == DYMU_OK;
   int rc = d->xp->preflight(ok, call_signature(nx, ny, goal_i, goal_j, K), st, err);
   if (rc) return rc == DYMU_ERR_ARG ? rc : abort_dist(d, rc);
+  // receive rows only after every rank accepted this solve (its signature pins nx): a
+  // rank whose arguments were rejected must not re-allocate (and re-publish) alone, or
+  // the next valid solve would wait for a buffer generation its peers never reach
+  if (d->xp->alloc(L, nx, err) != DYMU_OK)
+    return abort_dist(d, fail(err, "dymu_dist_solve", "receive rows: out of memory",
+                              DYMU_ERR_NOMEM));
   rc = d->xp->connect(err);
   if (rc) return abort_dist(d, rc);
   const Slab& s = L[0].s;

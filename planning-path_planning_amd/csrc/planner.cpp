@@ -596,12 +596,15 @@ void DyMuPathPlanner::streamTotalCost(Body&& body) const {
       if (th.joinable()) th.join();
     }
   } worker;
-  for (unsigned r0 = 0; r0 < ny_ && rc == DYMU_OK && !body_err; r0 += step) {
+  // body_err is written by the worker thread: it is read only after that thread's
+  // join (the join is the synchronisation), never while the worker may still run
+  for (unsigned r0 = 0; r0 < ny_ && rc == DYMU_OK; r0 += step) {
     const unsigned r1 = std::min(ny_, r0 + step);
     const uint64_t o = idx(0, r0);
     rc = dymu_memcpy_d2h(ctx_, &total_cost_[o], dT_ + o, sizeof(double) * (idx(0, r1) - o));
     if (worker.th.joinable()) worker.th.join();
-    if (rc == DYMU_OK && !body_err)
+    if (body_err) break;
+    if (rc == DYMU_OK)
       worker.th = std::thread([&body, &body_err, r0, r1] {
         try {
           body(r0, r1);

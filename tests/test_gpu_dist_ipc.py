@@ -37,8 +37,9 @@ def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank, 
         pre = None
         if bad_rank is not None:  # one rank passes an invalid slab / another K: all refuse
             bad = rank == bad_rank
+            wide = nx + 64 if bad and bad_kind == "nx" else nx  # a wider grid (and pitch)
             try:
-                solver.solve(0 if bad and bad_kind == "slab" else dF, dT, nx, nx, ny, goal[0],
+                solver.solve(0 if bad and bad_kind == "slab" else dF, dT, wide, wide, ny, goal[0],
                              goal[1], 3 if bad and bad_kind == "k" else 4)
                 pre = "solved"
             except dymu.DymuError as e:
@@ -99,11 +100,12 @@ def test_ipc_loop_across_processes_matches_oracle(dymu, oracle, world, nx, ny, g
     _run(oracle, world, nx, ny, goal, engine_kw)
 
 
-@pytest.mark.parametrize("bad_kind", ["slab", "k"])
+@pytest.mark.parametrize("bad_kind", ["slab", "k", "nx"])
 def test_ipc_preflight_rejects_on_every_rank(dymu, oracle, bad_kind):
-    """A rank-local argument error (a null speed slab on rank 1) or a rank passing
-    another K than its peers (which would run other rounds and leave them waiting)
-    fails every rank with DYMU_ERR_ARG through the collective pre-flight; the next
-    solve works."""
+    """A rank-local argument error (a null speed slab on rank 1), a rank passing
+    another K than its peers (which would run other rounds and leave them waiting),
+    or a rank passing a wider grid (whose receive rows must not be re-allocated and
+    re-published alone: ADVICE r3) fails every rank with DYMU_ERR_ARG through the
+    collective pre-flight; the next solves work."""
     _run(oracle, 3, 160, 200, (80, 100), dict(kernel=5, prio_target=8), bad_rank=1,
          bad_kind=bad_kind)
