@@ -56,17 +56,20 @@ def parse():
                     help="no per-launch events (roofline reported as null)")
     ap.add_argument("--backend", default="nccl",
                     help="N>1 only: 'nccl' (RCCL over xGMI) or 'gloo' (host-staged rehearsal)")
-    ap.add_argument("--exchange", default="native", choices=["native", "ipc", "python"],
-                    help="N>1: 'native' = C++ exchange loop with its own RCCL communicator "
-                         "(libdymu_dist); 'ipc' = the same loop over hipIpc-mapped rows and a "
-                         "shared-memory board (N ranks may share one GPU); 'python' = "
-                         "dymu.sharded over torch.distributed")
+    ap.add_argument("--exchange", default="native",
+                    choices=["native", "rccl", "ipc", "peer", "python"],
+                    help="N>1: 'native' = the C++ loop of libdymu_dist with the transport "
+                         "chosen on the node before the timed region: RCCL (or IPC when ranks "
+                         "share a GPU) vs the GPU-initiated peer transport; 'rccl' / 'ipc' / "
+                         "'peer' = that transport only (ipc / peer: N ranks may share one "
+                         "GPU); 'python' = dymu.sharded over torch.distributed")
     ap.add_argument("--passes-per-exchange", type=int, default=0,
                     help="passes per exchange round (0: the native loop at N>1 times K = "
                          "2/4/8 before the timed region and keeps the fastest, 4 at N=1; 16 for "
                          "the python loop; tools/vdist_rehearsal.py)")
     ap.add_argument("--no-k-tune", action="store_true",
-                    help="N>1 native loop: no K choice before the timed region (K = 4)")
+                    help="N>1 native loop: no transport / K choice before the timed region "
+                         "(RCCL or IPC, K = 4)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the row-slab path even at N=1 (exercises the RCCL code path)")
     ap.add_argument("--cpu-linear-size", type=int, default=2048,
@@ -451,9 +454,13 @@ def main():
                         "run to run)",
             "parallelism": ("single" if world == 1 and not args.sharded else
                             f"row-slab x{world} ("
-                            + {"native": "RCCL, native C++ loop",
-                               "ipc": "hipIpc rows + shared-memory board, native C++ loop"}
-                            .get(args.exchange, f"{args.backend}, torch.distributed loop") + ")"),
+                            + {"rccl": "RCCL P2P + all-reduce, native C++ loop",
+                               "ipc": "hipIpc rows + shared-memory board, native C++ loop",
+                               "peer": "GPU-initiated peer pushes with sequence tags + status "
+                                       "board, native C++ loop"}
+                            .get(tot.get("transport"), f"{args.backend}, torch.distributed loop")
+                            + ")"),
+            "transport": tot.get("transport"),
             "exchange_rounds_per_solve": tot.get("rounds", 0) / K,
             "passes_per_exchange": tot.get("passes_per_exchange"),
             "passes_per_solve": tot["passes"] / K,
@@ -472,7 +479,7 @@ def main():
         "roofline": roof,
         "cpu_baseline": None,
     }
-    if tot.get("k_autotune_ms"):  # untimed setup solves, one per candidate K (max over ranks)
+    if tot.get("k_autotune_ms"):  # untimed setup solves per candidate transport x K (max over ranks)
         line["config"]["k_autotune_ms"] = tot["k_autotune_ms"]
     if tot.get("variants"):
         line["variants"] = tot["variants"]

@@ -1,12 +1,15 @@
 """Multi-GPU leg of bench.py: one rank per GPU (torch.distributed.run), the
 16384^2 grid split in row slabs (dymu.slab_rows).
 
---exchange native (default): the C++ loop of libdymu_dist (dymu.dist.DistSolver)
-    with its own RCCL communicator on the engine's stream; torch.distributed
-    (gloo) only carries the communicator id, barriers and the max-over-ranks time.
---exchange ipc: the same C++ loop over its IPC transport (rows pushed into the
-    neighbours' hipIpc-mapped receive rows, counts through a /dev/shm board): runs
-    N ranks on ONE GPU, where RCCL refuses duplicate devices (rehearsal).
+--exchange native (default): the C++ loop of libdymu_dist (dymu.dist.DistSolver);
+    the transport is chosen on the node before the timed region among RCCL (its
+    own communicator on the engine's stream; only when every rank has its own GPU)
+    or IPC (ranks sharing a GPU) and the GPU-initiated peer transport (the pass
+    kernels push the boundary rows themselves), together with the passes per
+    round; torch.distributed (gloo) only carries the ids, barriers and the
+    max-over-ranks time.
+--exchange rccl | ipc | peer: that transport only (ipc / peer run N ranks on ONE
+    GPU too, where RCCL refuses duplicate devices).
 --exchange python: dymu.sharded.SlabSolver, the exchange loop in Python over
     torch.distributed ('nccl' = RCCL, or `--backend gloo` to rehearse N ranks on
     one GPU with host-staged rows).
@@ -48,8 +51,7 @@ def run(args):
     local = int(os.environ["LOCAL_RANK"])
     fake = getattr(args, "fake_cpu", False)
     exchange = getattr(args, "exchange", "native")
-    native = exchange in ("native", "ipc") and not fake
-    transport = "ipc" if exchange == "ipc" else "rccl"
+    native = exchange in ("native", "rccl", "ipc", "peer") and not fake
     K = args.passes_per_exchange or (4 if native else 16)
     backend = "gloo" if (native or fake) else getattr(args, "backend", "nccl")
     if fake:  # CPU rehearsal of the rank plumbing (tests): numpy stand-in engine
@@ -87,13 +89,23 @@ def run(args):
     if native:
         from dymu import dist as ddist
 
-        obj = [ddist.unique_id(transport) if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        solver = ddist.DistSolver(eng, dev_idx, obj[0], rank, world, transport=transport)
-        ranks_seen = solver.comm_count()  # what the transport itself sees
+        if exchange == "native":  # candidates, chosen on the node below
+            # RCCL refuses two ranks on one GPU: ranks sharing a GPU compare IPC instead
+            shared = world > max(torch.cuda.device_count(), 1) if not fake else True
+            cands = ["ipc" if shared else "rccl", "peer"] if world > 1 else ["rccl"]
+        else:
+            cands = [exchange]
+        solvers = {}
+        for tr in cands:
+            obj = [ddist.unique_id(tr) if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            solvers[tr] = ddist.DistSolver(eng, dev_idx, obj[0], rank, world, transport=tr)
+        transport = cands[0]
+        ranks_seen = min(sv.comm_count() for sv in solvers.values())  # what the transports see
 
-        def solve(k=None):
-            return solver.solve(F.data_ptr(), T_buf.data_ptr(), N, N, N, g[0], g[1], k or K)
+        def solve(k=None, tr=None):
+            return solvers[tr or transport].solve(F.data_ptr(), T_buf.data_ptr(), N, N, N, g[0],
+                                                  g[1], k or K)
     else:
         from dymu.sharded import SlabSolver
 
@@ -101,7 +113,7 @@ def run(args):
                             passes_per_exchange=K, check_every=4)
         ranks_seen = dist.get_world_size()
 
-        def solve(k=None):
+        def solve(k=None, tr=None):
             return solver.solve(F, T_buf, g[0], g[1])
     slabs = [None] * world
     dist.all_gather_object(slabs, [rank, row0, nrows])
@@ -109,28 +121,35 @@ def run(args):
         raise SystemExit(f"bench: {ranks_seen} ranks seen by the communicator, --gpus "
                          f"{args.gpus}")
     for _ in range(args.warmup):
-        solve()
+        for tr in (solvers if native else [None]):
+            solve(None, tr)
     k_tune = None
-    if native and world > 1 and not args.passes_per_exchange and not getattr(args, "no_k_tune", False):
-        # passes per exchange round, chosen on this node before the timed region: a round
-        # costs one P2P exchange (+ a 4-byte all-reduce every 4th), whose latency over
-        # xGMI the one-GPU rehearsal cannot see (K = 4 is best at <= 20 us
-        # per round, K = 6-8 above); every rank runs every candidate, the max over
-        # ranks of the best of two solves decides, and all ranks get the same K
+    tune = native and world > 1 and not getattr(args, "no_k_tune", False)
+    if tune:
+        # transport and passes per round, chosen on this node before the timed region: a
+        # round's exchange latency over xGMI is what the one-GPU rehearsal cannot see
+        # (DESIGN.md s5); every rank runs every candidate (transport x K, or the given K),
+        # the max over ranks of the best of two solves decides, and all ranks get the
+        # same choice.  Every candidate solve is a full solve of the same grid.
         k_tune = {}
-        for k in K_CANDIDATES:
-            best = float("inf")
-            for _ in range(2):
-                dist.barrier()
-                torch.cuda.synchronize()
-                t = time.perf_counter()
-                solve(k)
-                torch.cuda.synchronize()
-                el = torch.tensor([time.perf_counter() - t], dtype=torch.float64)
-                dist.all_reduce(el, op=dist.ReduceOp.MAX)
-                best = min(best, float(el.item()))
-            k_tune[k] = round(best * 1e3, 3)
-        K = min(k_tune, key=k_tune.get)  # identical on every rank (max-reduced times)
+        ks = [args.passes_per_exchange] if args.passes_per_exchange else list(K_CANDIDATES)
+        for tr in solvers:
+            k_tune[tr] = {}
+            for k in ks:
+                best = float("inf")
+                for _ in range(2):
+                    dist.barrier()
+                    torch.cuda.synchronize()
+                    t = time.perf_counter()
+                    solve(k, tr)
+                    torch.cuda.synchronize()
+                    el = torch.tensor([time.perf_counter() - t], dtype=torch.float64)
+                    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+                    best = min(best, float(el.item()))
+                k_tune[tr][k] = round(best * 1e3, 3)
+        # identical on every rank (max-reduced times)
+        transport, K = min(((tr, k) for tr in k_tune for k in k_tune[tr]),
+                           key=lambda c: k_tune[c[0]][c[1]])
     prof = not args.no_profile and not fake
     if not fake:
         eng.set_profiling(PROFILE_PERIOD if prof else 0)
@@ -166,6 +185,8 @@ def run(args):
     tot["slab_cells"] = nrows * N  # rank 0's slab: the roofline's per-launch bytes
     tot["ranks_seen"] = ranks_seen
     tot["passes_per_exchange"] = K
+    if native:
+        tot["transport"] = transport
     if k_tune is not None:
         tot["k_autotune_ms"] = k_tune
     tot["slabs"] = sorted(slabs)
@@ -174,7 +195,8 @@ def run(args):
     else:
         eng.set_profiling(0)
     if native:
-        solver.close()
+        for sv in solvers.values():
+            sv.close()
     tot["parity"] = self_check(eng, F, T_buf, N, row0, nrows, rank, world, g, args.obst, fake,
                                dt.device)
     if not fake:

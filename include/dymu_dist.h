@@ -17,6 +17,13 @@
  *   DYMU_DIST_IPC   rows pushed into the neighbours' hipIpc-mapped receive rows,
  *                   counts reduced through a POSIX shared-memory board; ranks of
  *                   one node, several per GPU allowed (dymu_dist_create_ipc)
+ *   DYMU_DIST_PEER  GPU-initiated: every round's first pass pushes its boundary
+ *                   rows' decreases straight into the neighbours' peer-mapped
+ *                   receive rows with a sequence tag and merges its own after
+ *                   theirs (dymu_dom_round_peer); no host step and no collective
+ *                   per round, the termination check (every 4th round) compares
+ *                   the ranks' posted status on the board; ranks of one node,
+ *                   several per GPU allowed (dymu_dist_create_peer)
  *   virtual         all ranks in one process (dymu_vdist_solve)
  *
  * This replaces, for a grid too large or too slow for one GPU, the reference's
@@ -43,6 +50,7 @@ extern "C" {
 #define DYMU_DIST_ID_BYTES 128 /* sizeof(ncclUniqueId) */
 #define DYMU_DIST_RCCL 0
 #define DYMU_DIST_IPC 1
+#define DYMU_DIST_PEER 2
 
 typedef struct dymu_dist dymu_dist;
 
@@ -65,7 +73,12 @@ int dymu_dist_destroy(dymu_dist* d);
 int dymu_dist_ipc_unique_id(unsigned char id[DYMU_DIST_ID_BYTES]);
 int dymu_dist_create_ipc(dymu_dist** out, dymu_ctx* ctx, int device,
                          const unsigned char id[DYMU_DIST_ID_BYTES], int rank, int world);
-/* DYMU_DIST_RCCL or DYMU_DIST_IPC */
+/* The peer transport: the same id (dymu_dist_ipc_unique_id) and collective
+ * creation; the boundary rows move GPU to GPU inside the pass kernels (DESIGN.md
+ * s5 "Peer transport").  Kernel-5 slabs, passes_per_exchange >= 2. */
+int dymu_dist_create_peer(dymu_dist** out, dymu_ctx* ctx, int device,
+                          const unsigned char id[DYMU_DIST_ID_BYTES], int rank, int world);
+/* DYMU_DIST_RCCL, DYMU_DIST_IPC or DYMU_DIST_PEER */
 int dymu_dist_transport(dymu_dist* d);
 
 /* Sharded solve of the global grid (nx x ny, goal (goal_i, goal_j) in global

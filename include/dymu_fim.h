@@ -193,6 +193,33 @@ int dymu_dom_round(dymu_ctx* ctx, uint32_t passes, const double* new_lo, const d
 int dymu_dom_post(dymu_ctx* ctx, const int32_t* d_src, uint32_t* seq);
 int dymu_dom_wait_post(dymu_ctx* ctx, uint32_t seq, double timeout_s, int32_t* value,
                        void* stream);
+/* Peer rounds (include/dymu_dist.h's GPU-initiated peer transport):
+ * dymu_dom_round whose first pass also PUSHES this rank's first / last owned row
+ * into the neighbours' receive rows (peer-mapped device memory) -- only the
+ * values below those last pushed -- and, from the pass's last workgroup, writes a
+ * sequence tag after them (system-scope release); the merge of the same pass reads
+ * this rank's own receive rows after their tags.  No host involvement and no wait
+ * on a neighbour: rows arrive whenever the neighbour's pass runs, and any mix of
+ * old and new values is a valid upper bound.  The round's second pass records in
+ * `ctl` the status a termination check needs: P (tiles queued for the round's two
+ * first passes), S per side (pushes that carried a decrease) and R per side (the
+ * smallest tag the round's merge read).  Kernel-5 domains, passes >= 2. */
+#define DYMU_PEER_CTL_BYTES 128
+typedef struct dymu_peer_links {
+  const double* recv[2];                 /* own receive rows: from rank-1 (0) / rank+1 (1) */
+  const unsigned long long* recv_tag[2]; /* their tags (written by the neighbours) */
+  double* send[2];                       /* the neighbours' receive rows for the first (0) /
+                                            last (1) owned row (peer-mapped), NULL = none */
+  unsigned long long* send_tag[2];       /* ... and their tags */
+  double* last[2];                       /* nx values last pushed per side (device) */
+  void* ctl;                             /* DYMU_PEER_CTL_BYTES of device memory */
+} dymu_peer_links;
+int dymu_dom_round_peer(dymu_ctx* ctx, uint32_t passes, const dymu_peer_links* links,
+                        void* stream);
+/* Arm a status post for the next launched pass: its block 0 stores the status of
+ * `ctl` (S0, S1, R0, R1) at dst[1..4], then (seq << 32) | P at dst[0] (release,
+ * system scope).  dst: device address of 5 words of host-coherent memory. */
+int dymu_dom_post_status(dymu_ctx* ctx, const void* ctl, unsigned long long* dst, uint32_t seq);
 /* Tiles queued for the next pass (synchronises `stream`). */
 int dymu_dom_pending(dymu_ctx* ctx, void* stream, uint64_t* pending);
 /* End the domain solve; fills stats (passes, visits, sweeps). */

@@ -57,6 +57,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -428,43 +429,50 @@ class RcclTransport final : public Transport {
 };
 
 // ---------------------------------------------------------------------------
-// IPC: rows pushed into the neighbours' hipIpc-mapped receive rows, counts
-// reduced through a board in POSIX shared memory (/dev/shm); one node, any
-// number of ranks per GPU.  Per round the host waits for its own push and for
-// both neighbours' (the exactness condition in the header comment); the
-// reduction is a host sum over the board.
+// The shared-memory board of the IPC and peer transports: one POSIX shared-memory
+// segment (/dev/shm) per communicator, one slot per rank.  Joining, the collective
+// pre-flight, the receive buffers' IPC handles, the per-check status and the abort
+// flag go through it; every host wait on it is bounded (DYMU_DIST_TIMEOUT_S) and
+// gives up at once when a rank has aborted.
 // ---------------------------------------------------------------------------
 struct BoardSlot {
   std::atomic<uint64_t> gen;       // generation of the published receive buffer
   std::atomic<uint64_t> cap;       // its elements per side
   std::atomic<uint64_t> pre[2];    // (solve << 1) | ok, in slot solve % 2
   std::atomic<uint64_t> sig[2];    // call_signature of that solve (stored before pre)
-  std::atomic<uint64_t> pushed;    // rounds whose push completed (running count)
-  std::atomic<uint64_t> check[4];  // ((check + 1) << 32) | count, slot check % 4
+  std::atomic<uint64_t> pushed;    // IPC: rounds whose push completed (running count)
+  std::atomic<uint64_t> check[4];  // IPC: ((check + 1) << 32) | count, slot check % 4
   std::atomic<uint64_t> joined;    // 1 once the rank opened the board
   std::atomic<uint64_t> aborted;   // 1 once the rank gave up the collective sequence
+  // peer: the status of check c in slot c % 4 -- P, S0, S1, R0, R1, then the tag
+  // (solve << 32) | (c + 1), stored last (release)
+  std::atomic<uint64_t> stat[4][6];
   unsigned char handle[HIP_IPC_HANDLE_SIZE];
-  unsigned char pad[256 - 13 * 8 - HIP_IPC_HANDLE_SIZE];
+  unsigned char pad[512 - 37 * 8 - HIP_IPC_HANDLE_SIZE];
 };
-static_assert(sizeof(BoardSlot) == 256, "board slot");
+static_assert(sizeof(BoardSlot) == 512, "board slot");
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "board atomics");
 
-class IpcTransport final : public Transport {
+class BoardTransport : public Transport {
  public:
   int rank = 0, world = 1;
   std::string name;
   bool owner = false;
   BoardSlot* board = nullptr;
   size_t board_bytes = 0;
-  double* recv = nullptr;  // [2 parity][2 side][cap], exported
-  uint64_t cap = 0;
-  uint64_t gen = 0;        // generation of recv
-  int32_t* d_cnt = nullptr;  // [2 parity] local counts
-  double* peer[2] = {nullptr, nullptr};  // rank-1's / rank+1's receive rows (mapped)
+  uint64_t solves = 0;
+  // the exported receive buffer and the neighbours' (mapped)
+  void* exported = nullptr;
+  uint64_t cap = 0, gen = 0;
+  void* peer[2] = {nullptr, nullptr};  // rank-1's / rank+1's exported buffer
   uint64_t peer_gen[2] = {0, 0}, peer_cap[2] = {0, 0};
-  uint64_t solves = 0, rounds = 0, checks = 0;
-  hipEvent_t ev = nullptr;
 
+  ~BoardTransport() override {
+    for (auto& p : peer)
+      if (p) (void)hipIpcCloseMemHandle(p);
+    if (board) munmap(board, board_bytes);
+    if (owner && !name.empty()) shm_unlink(name.c_str());
+  }
   // spin_until that also gives up as soon as any rank has aborted (its abort() after
   // an error): the peers fail at once instead of after the full timeout
   bool peer_aborted() const {
@@ -487,16 +495,6 @@ class IpcTransport final : public Transport {
   void abort() override {
     if (board) board[rank].aborted.store(1, std::memory_order_release);
   }
-
-  ~IpcTransport() override {
-    for (auto& p : peer)
-      if (p) (void)hipIpcCloseMemHandle(p);
-    if (recv) (void)hipFree(recv);
-    if (d_cnt) (void)hipFree(d_cnt);
-    if (ev) (void)hipEventDestroy(ev);
-    if (board) munmap(board, board_bytes);
-    if (owner && !name.empty()) shm_unlink(name.c_str());
-  }
   int open(const char* shm, int r, int w, std::string* err) {
     rank = r;
     world = w;
@@ -513,29 +511,16 @@ class IpcTransport final : public Transport {
     close(fd);
     if (p == MAP_FAILED) return fail(err, "mmap", std::strerror(errno), DYMU_ERR_STATE);
     board = static_cast<BoardSlot*>(p);
-    DHIP(err, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    DHIP(err, hipMalloc(&d_cnt, sizeof(int32_t) * 2));
+    DCALL(open_local(err));
     // collective, like ncclCommInitRank: every rank has joined on return
     board[rank].joined.store(1, std::memory_order_release);
     for (int q = 0; q < world; ++q)
       if (!spin_until([&] { return board[q].joined.load(std::memory_order_acquire) != 0; }))
-        return fail(err, "dymu_dist_create_ipc", "timed out waiting for the other ranks",
+        return fail(err, "dymu_dist_create", "timed out waiting for the other ranks",
                     DYMU_ERR_RCCL);
     return DYMU_OK;
   }
-  int alloc(std::vector<Local>& L, uint32_t nx, std::string* err) override {
-    if (cap < nx) {
-      if (recv) DHIP(err, hipFree(recv));
-      recv = nullptr;
-      cap = 0;
-      DHIP(err, hipMalloc(&recv, sizeof(double) * 4 * (uint64_t)nx));
-      cap = nx;
-      ++gen;
-    }
-    L[0].recv = recv + (rounds & 1) * 2 * cap;  // the parity the next merge reads
-    L[0].cap = cap;
-    return DYMU_OK;
-  }
+  virtual int open_local(std::string* err) = 0;
   int preflight(bool ok, uint64_t sig, hipStream_t, std::string* err) override {
     // One slot per solve parity: a rank that leaves this pre-flight may post the next
     // solve's before a slower peer has read this one's ok bit, and a single slot would
@@ -565,10 +550,12 @@ class IpcTransport final : public Transport {
     if (!same) return fail(err, "dymu_dist_solve", kSigMismatch, DYMU_ERR_ARG);
     return DYMU_OK;
   }
+  // publish `exported` (generation gen, cap elements per side) if it is new, and map
+  // both neighbours' current buffers
   int connect(std::string* err) override {
     if (board[rank].gen.load(std::memory_order_acquire) != gen) {  // publish a new buffer
       hipIpcMemHandle_t h;
-      DHIP(err, hipIpcGetMemHandle(&h, recv));
+      DHIP(err, hipIpcGetMemHandle(&h, exported));
       std::memcpy(board[rank].handle, &h, sizeof h);
       board[rank].cap.store(cap, std::memory_order_relaxed);
       board[rank].gen.store(gen, std::memory_order_release);
@@ -588,25 +575,75 @@ class IpcTransport final : public Transport {
       std::memcpy(&h, board[q].handle, sizeof h);
       void* p = nullptr;
       DHIP(err, hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-      peer[side] = static_cast<double*>(p);
+      peer[side] = p;
       peer_gen[side] = g;
       peer_cap[side] = board[q].cap.load(std::memory_order_relaxed);
     }
+    return DYMU_OK;
+  }
+  int ranks_seen() override {  // ranks that joined the board
+    int n = 0;
+    for (int q = 0; q < kMaxWorld; ++q) n += board[q].joined.load(std::memory_order_acquire) ? 1 : 0;
+    return n;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// IPC: rows pushed into the neighbours' hipIpc-mapped receive rows, counts
+// reduced through the board; one node, any number of ranks per GPU.  Per round
+// the host waits for its own push and for both neighbours' (the exactness
+// condition in the header comment); the reduction is a host sum over the board.
+// ---------------------------------------------------------------------------
+class IpcTransport final : public BoardTransport {
+ public:
+  double* recv = nullptr;  // [2 parity][2 side][cap], exported
+  int32_t* d_cnt = nullptr;  // [2 parity] local counts
+  uint64_t rounds = 0, checks = 0;
+  hipEvent_t ev = nullptr;
+
+  ~IpcTransport() override {
+    for (auto& p : peer)
+      if (p) (void)hipIpcCloseMemHandle(p);
+    peer[0] = peer[1] = nullptr;
+    if (recv) (void)hipFree(recv);
+    if (d_cnt) (void)hipFree(d_cnt);
+    if (ev) (void)hipEventDestroy(ev);
+  }
+  int open_local(std::string* err) override {
+    DHIP(err, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    DHIP(err, hipMalloc(&d_cnt, sizeof(int32_t) * 2));
+    return DYMU_OK;
+  }
+  int alloc(std::vector<Local>& L, uint32_t nx, std::string* err) override {
+    if (cap < nx) {
+      if (recv) DHIP(err, hipFree(recv));
+      recv = nullptr;
+      exported = nullptr;
+      cap = 0;
+      DHIP(err, hipMalloc(&recv, sizeof(double) * 4 * (uint64_t)nx));
+      exported = recv;
+      cap = nx;
+      ++gen;
+    }
+    L[0].recv = recv + (rounds & 1) * 2 * cap;  // the parity the next merge reads
+    L[0].cap = cap;
     return DYMU_OK;
   }
   int32_t* tot(int, int par) override { return d_cnt + par; }
   const int32_t* post_src(int par) override { return d_cnt + par; }
   int exchange(std::vector<Local>& L, uint32_t nx, hipStream_t st, std::string* err) override {
     Local& l = L[0];
+    double* const p0 = static_cast<double*>(peer[0]);
+    double* const p1 = static_cast<double*>(peer[1]);
     // push: my first row into rank-1's "from rank+1" row, my last into rank+1's
     // "from rank-1" row (ordered after this round's passes on my stream), both in
     // the receive parity of this round
     const uint64_t par = rounds & 1;
     if (l.s.lo)
-      DHIP(err, hipMemcpyAsync(peer[0] + (2 * par + 1) * peer_cap[0], l.s.row(0),
-                               sizeof(double) * nx, hipMemcpyDeviceToDevice, st));
+      DHIP(err, hipMemcpyAsync(p0 + (2 * par + 1) * peer_cap[0], l.s.row(0), sizeof(double) * nx,
+                               hipMemcpyDeviceToDevice, st));
     if (l.s.hi)
-      DHIP(err, hipMemcpyAsync(peer[1] + 2 * par * peer_cap[1], l.s.row(1), sizeof(double) * nx,
+      DHIP(err, hipMemcpyAsync(p1 + 2 * par * peer_cap[1], l.s.row(1), sizeof(double) * nx,
                                hipMemcpyDeviceToDevice, st));
     const uint64_t m = ++rounds;
     l.recv = recv + par * 2 * cap;  // the next round merges what the neighbours pushed now
@@ -639,10 +676,193 @@ class IpcTransport final : public Transport {
     *global = g;
     return DYMU_OK;
   }
-  int ranks_seen() override {  // ranks that joined the board
-    int n = 0;
-    for (int q = 0; q < kMaxWorld; ++q) n += board[q].joined.load(std::memory_order_acquire) ? 1 : 0;
-    return n;
+};
+
+// ---------------------------------------------------------------------------
+// Peer: GPU-initiated pushes, no host step per round (DESIGN.md s5 "Peer
+// transport").  Every round's first pass pushes the decreased values of this
+// rank's boundary rows straight into the neighbours' receive rows (peer-mapped,
+// over xGMI between GPUs) and then a per-link sequence tag; the merge of the same
+// pass reads this rank's receive rows after their tags (dymu_dom_round_peer).
+// Nothing waits for a neighbour: the host queues rounds back to back, and every
+// kCheckEvery-th round posts the status of the round before (P: tiles queued;
+// per link S: pushes that carried a decrease, R: the tag merged) into a
+// host-coherent ring, which the host copies onto the board one check late.
+// Termination (every rank decides alike from the same board entries): two
+// consecutive checks c-1, c in which every rank had P = 0, every link had R = S,
+// and no S moved between them.  Then every change ever made reached a boundary
+// row, was pushed (P = 0 means the round did nothing after its push), merged (R =
+// S) and improved nothing (P = 0 again), and nothing was pushed since -- the
+// global fixed point, checked like RCCL's zero count but without a collective.
+// The receive rows and tags live in fine-grained device memory
+// (hipDeviceMallocFinegrained: coherent while kernels run) and are read with
+// system-scope loads.
+// ---------------------------------------------------------------------------
+class PeerTransport final : public BoardTransport {
+ public:
+  // exported: [2 side][cap] receive rows, then 2 tags (own 128-byte line)
+  double* rx = nullptr;
+  unsigned long long* rtag = nullptr;
+  double* last = nullptr;      // [2 side][cap], local
+  void* ctl = nullptr;         // PeerCtl, local
+  unsigned long long* ring = nullptr;    // [kRing][8] words, host-coherent pinned
+  unsigned long long* d_ring = nullptr;  // its device address
+  static constexpr int kRing = 8;
+  bool fine = true;  // fine-grained receive rows (DYMU_PEER_COARSE=1: hipMalloc, A/B)
+
+  static uint64_t rx_bytes(uint64_t n) { return (sizeof(double) * 2 * n + 127) / 128 * 128 + 128; }
+  ~PeerTransport() override {
+    for (auto& p : peer)
+      if (p) (void)hipIpcCloseMemHandle(p);
+    peer[0] = peer[1] = nullptr;
+    if (rx) (void)hipFree(rx);
+    if (last) (void)hipFree(last);
+    if (ctl) (void)hipFree(ctl);
+    if (ring) (void)hipHostFree(ring);
+  }
+  int open_local(std::string* err) override {
+    if (const char* kv = std::getenv("DYMU_PEER_COARSE")) fine = std::atoi(kv) == 0;
+    DHIP(err, hipMalloc(&ctl, DYMU_PEER_CTL_BYTES));
+    DHIP(err, hipHostMalloc(&ring, sizeof(unsigned long long) * 8 * kRing,
+                            hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(ring, 0, sizeof(unsigned long long) * 8 * kRing);
+    void* d = nullptr;
+    DHIP(err, hipHostGetDevicePointer(&d, ring, 0));
+    d_ring = static_cast<unsigned long long*>(d);
+    return DYMU_OK;
+  }
+  int alloc(std::vector<Local>& L, uint32_t nx, std::string* err) override {
+    if (cap < nx) {
+      if (rx) DHIP(err, hipFree(rx));
+      if (last) DHIP(err, hipFree(last));
+      rx = nullptr;
+      last = nullptr;
+      exported = nullptr;
+      cap = 0;
+      void* p = nullptr;
+      if (fine)
+        DHIP(err, hipExtMallocWithFlags(&p, rx_bytes(nx), hipDeviceMallocFinegrained));
+      else
+        DHIP(err, hipMalloc(&p, rx_bytes(nx)));
+      rx = static_cast<double*>(p);
+      DHIP(err, hipMalloc(&last, sizeof(double) * 2 * (uint64_t)nx));
+      exported = rx;
+      cap = nx;
+      ++gen;
+    }
+    rtag = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(rx) + rx_bytes(cap) - 128);
+    L[0].recv = rx;
+    L[0].cap = cap;
+    return DYMU_OK;
+  }
+  // before the pre-flight (so no neighbour can push into them yet): receive rows and
+  // the values last pushed +inf, tags 0, counters 0 (rmin all ones)
+  int reset(hipStream_t st, std::string* err) {
+    DHIP(err, dymu::launch_fill_inf(rx, 0, (uint32_t)(2 * cap), 0, 1, st));
+    DHIP(err, hipMemsetAsync(rtag, 0, 128, st));
+    DHIP(err, dymu::launch_fill_inf(last, 0, (uint32_t)(2 * cap), 0, 1, st));
+    DHIP(err, hipMemsetAsync(ctl, 0, DYMU_PEER_CTL_BYTES, st));
+    DHIP(err, hipMemsetAsync(static_cast<char*>(ctl) + offsetof(dymu::PeerCtl, rmin), 0xFF,
+                             2 * sizeof(unsigned long long), st));
+    DHIP(err, hipStreamSynchronize(st));
+    return DYMU_OK;
+  }
+  // after connect(): every rank has reset its buffers before any rank starts pushing
+  // (a board barrier: the pushes of this solve follow it)
+  int ready(hipStream_t st, std::string* err) {
+    DCALL(reset(st, err));
+    board[rank].pushed.store(solves, std::memory_order_release);
+    for (int q = 0; q < world; ++q)
+      DCALL(wait([&] { return board[q].pushed.load(std::memory_order_acquire) >= solves; },
+                 "timed out waiting for the peers to reset", err));
+    return DYMU_OK;
+  }
+  int32_t* tot(int, int) override { return nullptr; }
+  const int32_t* post_src(int) override { return nullptr; }
+  int exchange(std::vector<Local>&, uint32_t, hipStream_t, std::string*) override { return DYMU_OK; }
+  int reduce(int, hipStream_t, std::string*) override { return DYMU_OK; }
+
+  struct Status {
+    uint64_t P = 0, S[2] = {0, 0}, R[2] = {0, 0};
+  };
+  // the rounds; the domain is live on entry
+  int run(Local& l, uint32_t nx, uint32_t ny, uint32_t K, hipStream_t st, std::string* err,
+          uint64_t* rounds_out) {
+    dymu_peer_links links{};
+    for (int side = 0; side < 2; ++side) {
+      const bool has = side == 0 ? l.s.lo : l.s.hi;
+      if (!has) continue;
+      links.recv[side] = rx + (uint64_t)side * cap;
+      links.recv_tag[side] = rtag + side;
+      // my first row goes into rank-1's "from rank+1" row (side 1 of its buffer), my
+      // last into rank+1's "from rank-1" row (side 0)
+      double* pb = static_cast<double*>(peer[side]);
+      const uint64_t pc = peer_cap[side];
+      links.send[side] = pb + (side == 0 ? pc : 0);
+      links.send_tag[side] = reinterpret_cast<unsigned long long*>(
+                                 reinterpret_cast<char*>(pb) + rx_bytes(pc) - 128) +
+                             (side == 0 ? 1 : 0);
+      links.last[side] = last + (uint64_t)side * cap;
+    }
+    links.ctl = ctl;
+    const uint64_t cap_r = max_rounds(nx, ny, K) + 2 * kCheckEvery;
+    const uint64_t solve = solves;
+    std::vector<Status> prev(world), cur(world);
+    bool prev_quiet = false;
+    uint64_t checks = 0, m = 0;
+    for (bool done = false; !done; ++m) {
+      if (m >= cap_r)
+        return fail(err, "dymu_dist_solve", "exchange-round cap reached", DYMU_ERR_NOT_CONVERGED);
+      int rc = dymu_dom_round_peer(l.ctx, K, &links, st);
+      if (rc) return fail(err, "dymu_dom_round_peer", dymu_last_error(l.ctx), rc);
+      if ((m % kCheckEvery) != kCheckEvery - 1) continue;
+      // this round's status is posted by the next launched pass into ring slot c
+      const uint64_t c = checks++;
+      unsigned long long* slot = ring + (c % kRing) * 8;
+      __atomic_store_n(slot, 0ull, __ATOMIC_RELEASE);
+      rc = dymu_dom_post_status(l.ctx, ctl, d_ring + (c % kRing) * 8, (uint32_t)(c + 1));
+      if (rc) return fail(err, "dymu_dom_post_status", dymu_last_error(l.ctx), rc);
+      if (c == 0) continue;
+      // the previous check's status (its post ran at the start of this round)
+      const uint64_t k = c - 1;
+      unsigned long long* ps = ring + (k % kRing) * 8;
+      uint64_t w0 = 0;
+      DCALL(wait([&] {
+              w0 = __atomic_load_n(ps, __ATOMIC_ACQUIRE);
+              return (w0 >> 32) == k + 1;
+            }, "timed out waiting for the device's status post", err));
+      BoardSlot& me = board[rank];
+      me.stat[k % 4][0].store((uint32_t)w0, std::memory_order_relaxed);
+      for (int q = 0; q < 4; ++q)
+        me.stat[k % 4][1 + q].store(__atomic_load_n(ps + 1 + q, __ATOMIC_RELAXED),
+                                    std::memory_order_relaxed);
+      me.stat[k % 4][5].store((solve << 32) | (k + 1), std::memory_order_release);
+      for (int q = 0; q < world; ++q) {
+        DCALL(wait([&] { return board[q].stat[k % 4][5].load(std::memory_order_acquire) ==
+                                ((solve << 32) | (k + 1)); },
+                   "timed out waiting for a peer's status", err));
+        Status& sq = cur[q];
+        sq.P = board[q].stat[k % 4][0].load(std::memory_order_relaxed);
+        for (int side = 0; side < 2; ++side) {
+          sq.S[side] = board[q].stat[k % 4][1 + side].load(std::memory_order_relaxed);
+          sq.R[side] = board[q].stat[k % 4][3 + side].load(std::memory_order_relaxed);
+        }
+      }
+      bool quiet = true, same = true;
+      for (int q = 0; q < world; ++q) {
+        quiet = quiet && cur[q].P == 0;
+        // link q -> q+1: q's pushes to rank+1 (side 1) against q+1's merges of rank-1 (side 0)
+        if (q + 1 < world) {
+          quiet = quiet && cur[q].S[1] == cur[q + 1].R[0] && cur[q + 1].S[0] == cur[q].R[1];
+        }
+        same = same && cur[q].S[0] == prev[q].S[0] && cur[q].S[1] == prev[q].S[1];
+      }
+      done = quiet && prev_quiet && same;
+      prev_quiet = quiet;
+      prev.swap(cur);
+    }
+    *rounds_out = m;
+    return DYMU_OK;
   }
 };
 
@@ -808,6 +1028,31 @@ int dymu_dist_create_ipc(dymu_dist** out, dymu_ctx* ctx, int device,
   return DYMU_OK;
 }
 
+int dymu_dist_create_peer(dymu_dist** out, dymu_ctx* ctx, int device,
+                          const unsigned char id[DYMU_DIST_ID_BYTES], int rank, int world) {
+  if (!out || !ctx || !id || world < 1 || world > kMaxWorld || rank < 0 || rank >= world)
+    return DYMU_ERR_ARG;
+  *out = nullptr;
+  char name[DYMU_DIST_ID_BYTES + 1];
+  std::memcpy(name, id, DYMU_DIST_ID_BYTES);
+  name[DYMU_DIST_ID_BYTES] = 0;
+  if (name[0] != '/' || std::strchr(name + 1, '/')) return DYMU_ERR_ARG;
+  dymu_dist* d = new_dist(ctx, device, rank, world, DYMU_DIST_PEER);
+  if (hipSetDevice(device) != hipSuccess) {
+    dymu_dist_destroy(d);
+    return DYMU_ERR_HIP;
+  }
+  auto x = std::make_unique<PeerTransport>();
+  const int rc = x->open(name, rank, world, &d->last_error);
+  d->xp = std::move(x);
+  if (rc) {
+    dymu_dist_destroy(d);
+    return rc;
+  }
+  *out = d;
+  return DYMU_OK;
+}
+
 int dymu_dist_destroy(dymu_dist* d) {
   if (!d) return DYMU_OK;
   (void)hipSetDevice(d->device);
@@ -856,11 +1101,19 @@ int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t 
                               DYMU_ERR_NOMEM));
   rc = d->xp->connect(err);
   if (rc) return abort_dist(d, rc);
+  auto* peer = d->kind == DYMU_DIST_PEER ? static_cast<PeerTransport*>(d->xp.get()) : nullptr;
+  if (peer && (rc = peer->ready(st, err)) != DYMU_OK) return abort_dist(d, rc);
   const Slab& s = L[0].s;
   rc = dymu_dom_begin(d->ctx, &s.dom, s.goal_local >= 0 ? goal_i : 0, s.goal_local, stream);
   if (rc) return abort_dist(d, fail(err, "dymu_dom_begin", dymu_last_error(d->ctx), rc));
+  if (peer && dymu_dom_round_supported(d->ctx, K) != 1) {
+    (void)dymu_dom_finish(d->ctx, stream, nullptr);
+    return abort_dist(d, fail(err, "dymu_dist_solve",
+                              "the peer transport needs kernel-5 slabs and K >= 2", DYMU_ERR_STATE));
+  }
   uint64_t rounds = 0;
-  rc = run_rounds(L, *d->xp, d->res, nx, ny, K, st, err, &rounds);
+  rc = peer ? peer->run(L[0], nx, ny, K, st, err, &rounds)
+            : run_rounds(L, *d->xp, d->res, nx, ny, K, st, err, &rounds);
   const int rf = dymu_dom_finish(d->ctx, stream, stats);
   if (rc) return abort_dist(d, rc);
   if (rf) return abort_dist(d, fail(err, "dymu_dom_finish", dymu_last_error(d->ctx), rf));

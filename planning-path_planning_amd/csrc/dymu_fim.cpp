@@ -65,6 +65,8 @@ struct dymu_ctx {
   // a post armed by dymu_dom_post for the next launched pass (sharded loop)
   const int32_t* arm_src = nullptr;
   uint32_t arm_seq = 0;
+  unsigned long long* arm_dst = nullptr;       // another post target (the peer status ring)
+  const unsigned long long* arm_ext = nullptr;  // ... with these 4 status words
   int prio_debug = 0;        // v4: print the state after the first N passes (DYMU_PRIO_DEBUG)
 
   // tile workspace
@@ -222,6 +224,8 @@ void dom_retire(dymu_ctx* c) {
   auto& D = c->dom;
   c->arm_seq = 0;  // a post armed for a pass that will not run
   c->arm_src = nullptr;
+  c->arm_dst = nullptr;
+  c->arm_ext = nullptr;
   if (!D.live) return;
   c->epoch_base = D.eb + (uint32_t)D.p + 4u;
   D.live = false;
@@ -427,11 +431,14 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st, uint32_t report_seq = 0)
       a.report = c->d_mail;
       a.report_seq = report_seq;
     } else if (c->arm_seq) {
-      a.report = c->d_mail;
+      a.report = c->arm_dst ? c->arm_dst : c->d_mail;
       a.report_seq = c->arm_seq;
       a.report_src = c->arm_src;
+      a.report_ext = c->arm_ext;
       c->arm_seq = 0;
       c->arm_src = nullptr;
+      c->arm_dst = nullptr;
+      c->arm_ext = nullptr;
     }
     a.pstat = (c->pass_stats && D.variant == 5 && c->d_pstat)
                   ? c->d_pstat + (p % kPassStatCap) * (uint64_t)kShards * kPsWords
@@ -468,6 +475,7 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st, uint32_t report_seq = 0)
     ++D.launches;
     a.report = nullptr;
     a.report_src = nullptr;
+    a.report_ext = nullptr;
     if (tr) {
       a.trace = nullptr;
       std::vector<unsigned long long> h((size_t)kTracePts * D.blocks);
@@ -587,6 +595,52 @@ int dom_round(dymu_ctx* c, uint64_t K, const double* lo, const double* hi, int32
   rc = dom_launch(c, 1, st);
   D.a.tot_prev = nullptr;
   D.a.tot_out = nullptr;
+  if (rc) return rc;
+  return dom_launch(c, K - 2, st);
+}
+
+// The peer round (include/dymu_fim.h dymu_dom_round_peer): dom_round whose first pass
+// also pushes the owned boundary rows into the neighbours' receive rows with a tag and
+// reads its own receive rows after their tags; the second pass records the status.
+int dom_round_peer(dymu_ctx* c, uint64_t K, const dymu_peer_links& L, hipStream_t st) {
+  auto& D = c->dom;
+  if (!dom_round_ok(c, K)) return DYMU_ERR_STATE;
+  if (!L.ctl || (L.recv[0] && !D.a.ghost_lo) || (L.recv[1] && !D.a.ghost_hi)) return DYMU_ERR_ARG;
+  for (int s = 0; s < 2; ++s)
+    if ((L.recv[s] && !L.recv_tag[s]) || (L.send[s] && (!L.send_tag[s] || !L.last[s])))
+      return DYMU_ERR_ARG;
+  PeerCtl* pc = static_cast<PeerCtl*>(L.ctl);
+  uint32_t* scratch = reinterpret_cast<uint32_t*>(c->d_scratch + 7);
+  PassArgs& a = D.a;
+  a.merge_lo = L.recv[0];
+  a.merge_hi = L.recv[1];
+  for (int s = 0; s < 2; ++s) {
+    a.merge_tag[s] = L.recv[s] ? L.recv_tag[s] : nullptr;
+    a.push_dst[s] = L.send[s];
+    a.push_tag[s] = L.send_tag[s];
+    a.push_last[s] = L.last[s];
+  }
+  a.peer = pc;
+  a.tot_save = scratch;
+  int rc = dom_launch(c, 1, st);
+  a.merge_lo = a.merge_hi = nullptr;
+  for (int s = 0; s < 2; ++s) {
+    a.merge_tag[s] = nullptr;
+    a.push_dst[s] = nullptr;
+    a.push_tag[s] = nullptr;
+    a.push_last[s] = nullptr;
+  }
+  a.tot_save = nullptr;
+  if (rc) {
+    a.peer = nullptr;
+    return rc;
+  }
+  a.tot_prev = scratch;
+  a.tot_out = reinterpret_cast<int32_t*>(&pc->pend);
+  rc = dom_launch(c, 1, st);
+  a.tot_prev = nullptr;
+  a.tot_out = nullptr;
+  a.peer = nullptr;
   if (rc) return rc;
   return dom_launch(c, K - 2, st);
 }
@@ -1393,10 +1447,31 @@ int dymu_dom_round(dymu_ctx* c, uint32_t passes, const double* new_lo, const dou
   return dom_round(c, passes, new_lo, new_hi, d_total, pick_stream(c, stream));
 }
 
+int dymu_dom_round_peer(dymu_ctx* c, uint32_t passes, const dymu_peer_links* links,
+                        void* stream) {
+  if (!c || !links) return DYMU_ERR_ARG;
+  static_assert(sizeof(PeerCtl) <= DYMU_PEER_CTL_BYTES, "peer control block");
+  HIPC(c, hipSetDevice(c->device));
+  return dom_round_peer(c, passes, *links, pick_stream(c, stream));
+}
+
+int dymu_dom_post_status(dymu_ctx* c, const void* ctl, unsigned long long* dst, uint32_t seq) {
+  if (!c || !ctl || !dst || seq == 0) return DYMU_ERR_ARG;
+  if (!c->dom.live) return DYMU_ERR_STATE;
+  const PeerCtl* pc = static_cast<const PeerCtl*>(ctl);
+  c->arm_src = reinterpret_cast<const int32_t*>(&pc->pend);
+  c->arm_ext = pc->ext;
+  c->arm_dst = dst;
+  c->arm_seq = seq;
+  return DYMU_OK;
+}
+
 int dymu_dom_post(dymu_ctx* c, const int32_t* d_src, uint32_t* seq) {
   if (!c || !d_src || !seq) return DYMU_ERR_ARG;
   if (!c->d_mail || !c->dom.live) return DYMU_ERR_STATE;
   if (++c->mail_seq == 0) c->mail_seq = 1;
+  c->arm_dst = nullptr;
+  c->arm_ext = nullptr;
   c->arm_src = d_src;
   c->arm_seq = c->mail_seq;
   *seq = c->mail_seq;

@@ -23,6 +23,20 @@ struct ProbeCells {
   int n;
 };
 
+// Counters of the peer rounds (dymu_dom_round_peer, DESIGN.md s5 "Peer transport"),
+// in the rank's own device memory, zeroed at the start of a solve (rmin: all ones).
+// side 0 = the link to rank-1, side 1 = the link to rank+1.
+struct PeerCtl {
+  uint32_t done[2];               // workgroups that finished this pass's push of a side
+  uint32_t changed[2];            // some pushed column of the side decreased this pass
+  unsigned long long sent[2];     // S: pushes that carried a decrease (= the tags written)
+  unsigned long long rmin[2];     // smallest tag a merging workgroup read this round
+  unsigned long long merged[2];   // R: the tag of the last complete merge (status pass)
+  uint32_t pend;                  // P: tiles queued for the round's first + second pass
+  uint32_t pad;
+  unsigned long long ext[4];      // the posted status: S0, S1, R0, R1 (with pend)
+};
+
 struct PassArgs {
   const double* F;  // speed, pitch ld
   double* T;        // total cost, pitch ld (row -1 / row ny are ghost rows when flagged)
@@ -70,6 +84,9 @@ struct PassArgs {
   unsigned long long* report;
   uint32_t report_seq;
   const int32_t* report_src;  // post *report_src instead of the pass's count (sharded loop)
+  // with report_src: these 4 words are stored at report[1..4] before the (seq | count)
+  // word at report[0] (a fresh slot per post: the peer loop's status ring)
+  const unsigned long long* report_ext;
   // priority kernels, with report: bit 31 of the posted count is set when every queued
   // tile's key (min key of the input list) exceeds the largest T over these cells -- they
   // are final (the early exit of dymu_solve_until_device); n = 0: off
@@ -82,6 +99,17 @@ struct PassArgs {
   uint32_t* tot_save;       // block 0 stores the pass's count here ...
   const uint32_t* tot_prev;  // ... and a later pass stores *tot_prev + its count
   int32_t* tot_out;          //     into *tot_out (the round's termination count)
+  // peer rounds (dymu_dom_round_peer): the merge reads merge_tag[s] (the sequence tag
+  // the neighbour writes after its push, system scope) before its share of the row,
+  // and the pass pushes the owned first (0) / last (1) row's decreased values into the
+  // neighbour's receive row push_dst[s] (peer-mapped) and, from the last workgroup,
+  // the new tag into push_tag[s]; push_last[s] holds the values last pushed.  With
+  // peer set, the status pass (tot_out) also records S / R in *peer.
+  const unsigned long long* merge_tag[2];
+  double* push_dst[2];
+  unsigned long long* push_tag[2];
+  double* push_last[2];
+  PeerCtl* peer;
   // ---- kernel 5: edge columns (required) ----
   // ec[t * 32 + 0..15] = column 0 (W edge) of tile t's T, ec[t * 32 + 16..31] = column
   // 15 (E edge): an interior tile reads its W / E halo as ONE 128-byte line of its

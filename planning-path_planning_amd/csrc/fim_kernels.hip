@@ -350,8 +350,79 @@ __device__ __forceinline__ void report_pending(const PassArgs& a, uint32_t n_act
       }
       if (*a.minkey_in > tmax) v |= 0x80000000u;
     }
+    if (a.report_ext) {  // the status words first, then the word the host polls
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        __hip_atomic_store(a.report + 1 + k, a.report_ext[k], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.report, ((unsigned long long)a.report_seq << 32) | v, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
     __hip_atomic_store(a.report, ((unsigned long long)a.report_seq << 32) | v, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// ---- peer rounds (dymu_dom_round_peer; DESIGN.md s5 "Peer transport") ----
+// The status pass of a round (block 0, thread 0): R per side = the smallest tag the
+// round's merging workgroups read (kept when no workgroup merged that side), then
+// the status (S0, S1, R0, R1) beside P (pend) for the next check's post.
+__device__ __forceinline__ void peer_status(PeerCtl* pc) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const unsigned long long rm = pc->rmin[s];
+    if (rm != ~0ull) pc->merged[s] = rm;
+    pc->rmin[s] = ~0ull;
+  }
+  pc->ext[0] = pc->sent[0];
+  pc->ext[1] = pc->sent[1];
+  pc->ext[2] = pc->merged[0];
+  pc->ext[3] = pc->merged[1];
+}
+
+// One wave per workgroup pushes the workgroup's column share [m0, m1) of the owned
+// first / last row into the neighbour's receive row: only values below the last
+// pushed ones (values only decrease), stored at system scope over xGMI (or into
+// another process's buffer on the same GPU).  The workgroup then counts itself done;
+// the last one of the pass, if any column of the side decreased, bumps S and writes
+// it as the neighbour's tag after a system-scope fence -- every workgroup's values
+// are visible before the tag that covers them.  No wait on the neighbour anywhere.
+__device__ __forceinline__ void peer_push(const PassArgs& a, int64_t m0, int64_t m1, int lane) {
+  PeerCtl* pc = a.peer;
+  for (int s = 0; s < 2; ++s) {
+    double* dst = a.push_dst[s];
+    if (!dst) continue;
+    const double* row = a.T + (s == 0 ? 0 : (a.ny - 1) * a.ld);
+    double* last = a.push_last[s];
+    bool ch = false;
+    for (int64_t k0 = m0; k0 < m1; k0 += 64) {
+      const int64_t k = k0 + lane;
+      if (k < m1) {
+        const double v = row[k];
+        if (v < last[k]) {
+          last[k] = v;
+          __hip_atomic_store(dst + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          ch = true;
+        }
+      }
+    }
+    const bool any = __any(ch);
+    __threadfence_system();  // this wave's pushed values before its done count
+    if (lane == 0) {
+      if (any) __hip_atomic_fetch_or(&pc->changed[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t prev =
+          __hip_atomic_fetch_add(&pc->done[s], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == gridDim.x - 1u) {  // the pass's last workgroup for this side
+        __hip_atomic_store(&pc->done[s], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_exchange(&pc->changed[s], 0u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT)) {
+          const unsigned long long S = pc->sent[s] + 1ull;
+          pc->sent[s] = S;
+          __threadfence_system();
+          __hip_atomic_store(a.push_tag[s], S, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+    }
   }
 }
 
@@ -1206,6 +1277,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       report_pending(a, n_active);
       if (a.tot_save) *a.tot_save = n_active;
       if (a.tot_out) *a.tot_out = (int32_t)(*a.tot_prev + n_active);
+      if (a.peer && a.tot_out) peer_status(a.peer);
     }
   }
 
@@ -1321,7 +1393,8 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     }
     first = false;
   }
-  if (a.merge_lo || a.merge_hi) {  // uniform; the first wave out of the loop merges
+  const bool pushes = a.push_dst[0] || a.push_dst[1];  // peer rounds: this pass pushes
+  if (a.merge_lo || a.merge_hi || pushes) {  // uniform; the first wave out of the loop merges
     uint32_t mine = 0;
     if (lane == 0) mine = atomicAdd(&s_merge, 1u) == 0u;
     if (__builtin_amdgcn_readfirstlane(mine)) {
@@ -1334,13 +1407,26 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       for (int side = 0; side < 2; ++side) {
         const double* src = side == 0 ? a.merge_lo : a.merge_hi;
         if (!src) continue;
+        const bool tagged = a.merge_tag[side] != nullptr;  // peer rounds: a neighbour writes src
+        if (tagged && m0 < m1 && lane == 0) {
+          // the tag first: the rows of every push up to it are complete (the pusher's
+          // release); R = the smallest tag any workgroup read (status pass)
+          const unsigned long long t = __hip_atomic_load(a.merge_tag[side], __ATOMIC_ACQUIRE,
+                                                         __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_fetch_min(&a.peer->rmin[side], t, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+        }
         double* gh = a.T + (side == 0 ? -a.ld : a.ny * a.ld);
         const uint32_t trow = side == 0 ? 0u : (uint32_t)(a.nty - 1);
         for (int64_t k0 = m0; k0 < m1; k0 += 64) {
           const int64_t k = k0 + lane;
           double w = dinf();
           if (k < m1) {
-            const double v = src[k];
+            // a row another process's kernel writes while this one runs: system-scope
+            // loads (any mix of old and new 8-byte values is a valid upper bound)
+            const double v = tagged ? __hip_atomic_load(const_cast<double*>(src) + k,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                    : src[k];
             if (v < gh[k]) {
               gh[k] = v;
               w = v;
@@ -1352,6 +1438,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
             enqueue(trow * (uint32_t)a.ntx + (uint32_t)(k >> 4), dbits(w));
         }
       }
+      if (pushes) peer_push(a, m0, m1, lane);
     }
   }
   if (trace && tid == 0) trace[3] = __builtin_amdgcn_s_memrealtime();

@@ -8,6 +8,9 @@ mailbox so the host never drains the device queue.  One loop, three transports:
   "rccl"  grouped ncclSend/ncclRecv over xGMI + ncclAllReduce (one GPU per rank)
   "ipc"   rows pushed into the neighbours' hipIpc-mapped receive rows, counts
           reduced through a /dev/shm board (ranks of one node, may share a GPU)
+  "peer"  the rows pushed by the pass kernels themselves into the neighbours'
+          peer-mapped receive rows with sequence tags; no host step per round,
+          termination from the ranks' posted status on the board
   vdist_solve: every rank in this process (device-to-device copies).
 
 torch.distributed only carries the control plane here (the 128-byte id,
@@ -37,6 +40,7 @@ DIST_SYMBOLS = {
                                 ctypes.POINTER(DymuStats)]),
     "dymu_dist_ipc_unique_id": (_i32, [ctypes.c_char_p]),
     "dymu_dist_create_ipc": (_i32, [ctypes.POINTER(_vp), _vp, _i32, ctypes.c_char_p, _i32, _i32]),
+    "dymu_dist_create_peer": (_i32, [ctypes.POINTER(_vp), _vp, _i32, ctypes.c_char_p, _i32, _i32]),
     "dymu_dist_transport": (_i32, [_vp]),
     "dymu_dist_last_error": (ctypes.c_char_p, [_vp]),
     "dymu_dist_comm_count": (_i32, [_vp, ctypes.POINTER(ctypes.c_int)]),
@@ -61,15 +65,15 @@ def load_dist() -> ctypes.CDLL:
     return _dl
 
 
-TRANSPORTS = ("rccl", "ipc")
+TRANSPORTS = ("rccl", "ipc", "peer")
 
 
 def unique_id(transport: str = "rccl") -> bytes:
     """A fresh transport id (call on rank 0, broadcast the bytes): the RCCL
-    communicator id, or the IPC board's shared-memory name."""
+    communicator id, or the shared-memory board's name (IPC and peer transports)."""
     buf = ctypes.create_string_buffer(ID_BYTES)
     lib = load_dist()
-    fn = lib.dymu_dist_ipc_unique_id if transport == "ipc" else lib.dymu_dist_unique_id
+    fn = lib.dymu_dist_ipc_unique_id if transport in ("ipc", "peer") else lib.dymu_dist_unique_id
     _check(fn(buf))
     return buf.raw
 
@@ -85,8 +89,8 @@ class DistSolver:
         self.rank, self.world = rank, world
         self.transport = transport
         self.h = _vp()
-        create = (self._lib.dymu_dist_create_ipc if transport == "ipc"
-                  else self._lib.dymu_dist_create)
+        create = {"ipc": self._lib.dymu_dist_create_ipc,
+                  "peer": self._lib.dymu_dist_create_peer}.get(transport, self._lib.dymu_dist_create)
         rc = create(ctypes.byref(self.h), engine.ctx, device, uid, rank, world)
         if rc != 0:
             raise DymuError(rc, f"dymu_dist_create ({transport} transport)")

@@ -71,16 +71,17 @@ def test_bench_world_mismatch_fails():
 
 
 @pytest.mark.gpu
-def test_bench_gpus2_ipc_one_gpu_self_check():
+def test_bench_gpus2_one_gpu_transport_choice_self_check():
     """The multi-GPU bench path end to end on the one GPU of a test box: `bench.py
-    --gpus 2 --exchange ipc` spawns two ranks (torch.distributed.run), both on
-    device 0, runs the native round loop over the IPC transport, and its
-    self-check (slab residual, ghost rows, sum / count vs a single-GPU solve) must
-    pass -- the code the driver's N-GPU run executes, with RCCL's P2P swapped for
-    IPC because RCCL refuses two ranks on one GPU."""
+    --gpus 2` spawns two ranks (torch.distributed.run), both on device 0, and --
+    before the timed region -- times every candidate transport x passes per round:
+    IPC (RCCL refuses two ranks on one GPU; on a node with a GPU per rank the
+    candidate is RCCL) against the GPU-initiated peer transport.  The line carries
+    both candidates' times and the choice, and the run's self-check (slab residual,
+    ghost rows, sum / count vs a single-GPU solve) must pass -- the code the
+    driver's N-GPU run executes."""
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
-                          "--exchange", "ipc", "--size", "2048", "--steps", "2", "--warmup", "1",
-                          "--cpu-sample", "0"],
+                          "--size", "2048", "--steps", "2", "--warmup", "1", "--cpu-sample", "0"],
                          env=_env(DYMU_DIST_TIMEOUT_S="60"), cwd=ROOT, capture_output=True,
                          text=True, timeout=280)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -89,11 +90,29 @@ def test_bench_gpus2_ipc_one_gpu_self_check():
     par = rec["parity"]
     assert par["ok"] and par["ghost_max_abs_diff"] == 0 and par["mismatched_cells"] == 0
     assert par["finite_cells"] == par["finite_cells_single"] > 0.9 * 2048 * 2048
-    # the passes-per-exchange choice made before the timed region: every candidate timed,
-    # the fastest kept (bench_sharded.K_CANDIDATES)
+    # every candidate timed, the fastest (transport, K) kept (bench_sharded.K_CANDIDATES)
     tune = rec["config"]["k_autotune_ms"]
-    assert sorted(int(k) for k in tune) == [2, 4, 8] and min(tune.values()) > 0
-    assert rec["config"]["passes_per_exchange"] == int(min(tune, key=tune.get))
+    assert sorted(tune) == ["ipc", "peer"]
+    for tr in tune:
+        assert sorted(int(k) for k in tune[tr]) == [2, 4, 8] and min(tune[tr].values()) > 0
+    best = min(((tr, int(k)) for tr in tune for k in tune[tr]),
+               key=lambda c: tune[c[0]][str(c[1])])
+    assert (rec["config"]["transport"], rec["config"]["passes_per_exchange"]) == best
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exchange", ["ipc", "peer"])
+def test_bench_gpus2_fixed_transport_self_check(exchange):
+    """`--exchange ipc|peer` runs that transport only, with its self-check."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--exchange", exchange, "--size", "1024", "--steps", "2", "--warmup",
+                          "1", "--cpu-sample", "0", "--passes-per-exchange", "4"],
+                         env=_env(DYMU_DIST_TIMEOUT_S="60"), cwd=ROOT, capture_output=True,
+                         text=True, timeout=280)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["config"]["transport"] == exchange and rec["parity"]["ok"]
+    assert rec["config"]["passes_per_exchange"] == 4
 
 
 @pytest.mark.gpu

@@ -14,7 +14,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank, bad_kind):
+def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank, bad_kind,
+            transport):
     os.environ.setdefault("DYMU_DIST_TIMEOUT_S", "90")
     import sys
     import time
@@ -28,7 +29,7 @@ def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank, 
     try:
         row0, nrows = dymu.slab_rows(ny, world, rank)
         eng = dymu.Engine(device=0, **engine_kw)
-        solver = dist.DistSolver(eng, 0, uid, rank, world, transport="ipc")
+        solver = dist.DistSolver(eng, 0, uid, rank, world, transport=transport)
         marks.append(("joined", round(time.monotonic() - t0, 2)))
         seen = solver.comm_count()
         dF = eng.alloc(8 * nrows * nx)
@@ -58,16 +59,18 @@ def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank, 
         out_q.put((rank, 0, None, None, 0, None, f"rank {rank}: {e!r} {marks}"))
 
 
-def _run(oracle, world, nx, ny, goal, engine_kw, bad_rank=None, bad_kind="slab"):
+def _run(oracle, world, nx, ny, goal, engine_kw, bad_rank=None, bad_kind="slab", transport="ipc",
+         obst=0.03):
     import multiprocessing as mp
     from dymu import dist
 
-    F = oracle.synth_speed(nx, ny, seed=71, obst_frac=0.03, obst_seed=73, goal=goal)
-    uid = dist.unique_id("ipc")
+    F = oracle.synth_speed(nx, ny, seed=71, obst_frac=obst, obst_seed=73, goal=goal)
+    uid = dist.unique_id(transport)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker,
-                         args=(r, world, uid, nx, ny, goal, F, q, engine_kw, bad_rank, bad_kind))
+                         args=(r, world, uid, nx, ny, goal, F, q, engine_kw, bad_rank, bad_kind,
+                               transport))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -84,7 +87,10 @@ def _run(oracle, world, nx, ny, goal, engine_kw, bad_rank=None, bad_kind="slab")
         assert min(rounds) >= 2
         if bad_rank is not None:
             assert pre == -1, f"rank {rank}: pre-flight gave {pre}"
-    assert len({tuple(r[3]) for r in res}) == 1  # every rank ran the same rounds
+    # every rank ran the same rounds (lock-step transports); the peer ranks all stop at
+    # the same check but may have queued a different number of rounds by then
+    if transport != "peer":
+        assert len({tuple(r[3]) for r in res}) == 1
     Tref, _ = oracle.fmm(F, goal)
     assert np.array_equal(np.isinf(T), np.isinf(Tref))
     fin = np.isfinite(Tref)
@@ -109,3 +115,26 @@ def test_ipc_preflight_rejects_on_every_rank(dymu, oracle, bad_kind):
     collective pre-flight; the next solves work."""
     _run(oracle, 3, 160, 200, (80, 100), dict(kernel=5, prio_target=8), bad_rank=1,
          bad_kind=bad_kind)
+
+
+# The GPU-initiated peer transport (dymu_dist_create_peer, DESIGN.md s5 "Peer
+# transport"): the pass kernels push their boundary rows' decreases into the
+# neighbours' receive rows with sequence tags, no host step per round; termination
+# from the ranks' posted status.  Same processes-on-one-GPU harness and oracle.
+@pytest.mark.parametrize("world,nx,ny,goal,engine_kw,obst", [
+    (2, 257, 300, (250, 3), dict(kernel=5, prio_target=8), 0.03),
+    (3, 300, 420, (150, 200), dict(kernel=5, prio_target=16), 0.03),   # goal in the middle
+    (4, 512, 640, (40, 600), dict(kernel=5), 0.05),                     # 4 ranks, far goal
+], ids=["w2", "w3-middle", "w4"])
+def test_peer_loop_across_processes_matches_oracle(dymu, oracle, world, nx, ny, goal, engine_kw,
+                                                   obst):
+    _run(oracle, world, nx, ny, goal, engine_kw, transport="peer", obst=obst)
+
+
+@pytest.mark.parametrize("bad_kind", ["slab", "nx"])
+def test_peer_preflight_rejects_on_every_rank(dymu, oracle, bad_kind):
+    """The peer transport's pre-flight (the same board as IPC): a rank-local error
+    fails every rank with DYMU_ERR_ARG; the following solves reset the receive rows
+    and match the oracle."""
+    _run(oracle, 3, 160, 200, (80, 100), dict(kernel=5, prio_target=8), bad_rank=1,
+         bad_kind=bad_kind, transport="peer")
