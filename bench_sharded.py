@@ -95,12 +95,25 @@ def run(args):
             cands = ["ipc" if shared else "rccl", "peer"] if world > 1 else ["rccl"]
         else:
             cands = [exchange]
-        solvers = {}
+        solvers, dropped = {}, {}
         for tr in cands:
             obj = [ddist.unique_id(tr) if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
-            solvers[tr] = ddist.DistSolver(eng, dev_idx, obj[0], rank, world, transport=tr)
-        transport = cands[0]
+            try:
+                solvers[tr] = ddist.DistSolver(eng, dev_idx, obj[0], rank, world, transport=tr)
+                ok = 1
+            except dymu.DymuError as e:
+                dropped[tr] = str(e)
+                ok = 0
+            if not _all_ok(ok) and len(cands) > 1:  # a candidate that fails anywhere is dropped
+                dropped.setdefault(tr, "failed on another rank")
+                if tr in solvers:
+                    solvers.pop(tr).close()
+            elif not ok:
+                raise SystemExit(f"bench: transport {tr}: {dropped[tr]}")
+        if not solvers:
+            raise SystemExit(f"bench: no transport works: {dropped}")
+        transport = next(iter(solvers))
         ranks_seen = min(sv.comm_count() for sv in solvers.values())  # what the transports see
 
         def solve(k=None, tr=None):
@@ -121,8 +134,21 @@ def run(args):
         raise SystemExit(f"bench: {ranks_seen} ranks seen by the communicator, --gpus "
                          f"{args.gpus}")
     for _ in range(args.warmup):
-        for tr in (solvers if native else [None]):
-            solve(None, tr)
+        for tr in (list(solvers) if native else [None]):
+            if native and len(solvers) > 1:
+                # a candidate whose solve fails on any rank (its peers fail fast through the
+                # board's abort flag) is dropped on every rank before the timed region
+                try:
+                    solve(None, tr)
+                    ok = 1
+                except dymu.DymuError as e:
+                    dropped[tr], ok = str(e), 0
+                if not _all_ok(ok):
+                    dropped.setdefault(tr, "failed on another rank")
+                    solvers.pop(tr).close()
+                    transport = next(iter(solvers))
+            else:
+                solve(None, tr)
     k_tune = None
     tune = native and world > 1 and not getattr(args, "no_k_tune", False)
     if tune:
@@ -187,6 +213,8 @@ def run(args):
     tot["passes_per_exchange"] = K
     if native:
         tot["transport"] = transport
+        if dropped:
+            tot["transports_dropped"] = dropped
     if k_tune is not None:
         tot["k_autotune_ms"] = k_tune
     tot["slabs"] = sorted(slabs)
@@ -205,6 +233,13 @@ def run(args):
     if rank != 0:
         return None
     return float(dt.item()), tot, kern_ms, kern_n, st
+
+
+def _all_ok(ok):
+    """every rank's flag (gloo all-reduce MIN)"""
+    t = torch.tensor([ok], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
 
 
 RTOL = 1e-12  # SURVEY s8(c) / DESIGN.md s3 tolerance
