@@ -30,11 +30,15 @@
 //     the CLOSED values), every other cell +inf; ties between equal total
 //     costs may order differently from the reference's insertion order.
 //   * the node-pointer members are accessors returning snapshots:
-//     globalNarrowband(), globalGoal(), localAgent(); global_propagated_nodes
-//     and the local band lists are not exposed (every finite node is
-//     propagated), nor are the per-node steps of the loops the library runs
-//     whole (propagateGlobalNode, propagateLocalNode, minCostLocalNode,
-//     maxRiskNode, propagateRisk, setHorizonCost).
+//     globalNarrowband(), globalPropagatedNodes(), globalGoal(), localAgent(),
+//     localNarrowband(), localExpandableObstacles(), localPropagatedNodes(); a
+//     node's public `state` is written through setGlobalNodeState.  The per-node
+//     steps of the loops the library runs whole are there too, by grid index or
+//     snapshot (propagateGlobalNode, maxRiskNode, propagateRisk,
+//     propagateLocalNode, minCostLocalNode x2), so a caller can drive the
+//     reference's loops itself.  setHorizonCost (src/DyMu.hpp:555) is declared
+//     but defined nowhere in the reference (a caller cannot link it there); it
+//     is not provided.
 //   * a start or goal on the border returns false instead of dereferencing
 //     NULL (reference :416-417, :430-431).
 #pragma once
@@ -155,6 +159,22 @@ class DyMuPathPlanner {
   std::optional<globalNode> minCostGlobalNode();
   // :487-498: the band holds only the goal (total cost 0)
   void resetGlobalNarrowBand();
+  // :500-546: the reference update of node (i, j) from its nb4's current total costs
+  // (a NULL neighbour: the other one alone; C from the node's cost, hazard and
+  // trafficability); a lower value is taken, and a node whose total cost was +inf
+  // joins the band (appended: insertion order, like the reference's vector) and the
+  // propagated list.  Host arithmetic on the host copy of the map: for callers that
+  // drive the propagation node by node; the solves run on the GPU.
+  void propagateGlobalNode(unsigned i, unsigned j);
+  void propagateGlobalNode(const globalNode& n);
+  // the reference's public globalNode::state written by a caller (its FMM loop sets
+  // CLOSED after each minCostGlobalNode); the next solve recomputes every state
+  void setGlobalNodeState(unsigned i, unsigned j, node_state s);
+  // global_propagated_nodes (:447): every node with a finite total cost -- grid-index
+  // order, then those added by propagateGlobalNode in insertion order.  (At 16384^2
+  // after a full solve that is ~2.6e8 snapshots: globalPropagatedCount first.)
+  std::vector<globalNode> globalPropagatedNodes();
+  uint64_t globalPropagatedCount();
   // :731-784 / L:979-1023: the normalised descent direction at a node (the
   // reference's gradientNode(globalNode*) / gradientNode(localNode*))
   void gradientNode(unsigned i, unsigned j, double& dnx, double& dny) const;
@@ -180,6 +200,30 @@ class DyMuPathPlanner {
   void createLocalMap(unsigned i, unsigned j);                 // :97-148 (as subdivide)
   // L:851-869: the step toward the nb4 sub-cell of lowest deviation
   base::Waypoint computeLocalWaypointDijkstra(const localNode& lNode);
+  // the per-node steps of expandRisk / computeLocalPropagation (L:525-576, L:700-805):
+  // maxRiskNode pops local_expandable_obstacles by the reference's rule (the front,
+  // unless it is below 1 and a later entry is higher: then the first such), nullopt
+  // when empty; propagateRisk / propagateLocalNode apply the risk / deviation update
+  // to a sub-cell and queue it like the reference; minCostLocalNode pops the band
+  // node of lowest deviation (SWEEPING, :752-775) or deviation + distance to
+  // reachNode (CONSERVATIVE, :777-805), first strict minimum in insertion order
+  // the reference's localNode::nb4List[d] (src/DyMu.hpp:52; d: 0 (i,j-1), 1 (i-1,j),
+  // 2 (i+1,j), 3 (i,j+1)): nullopt where the reference holds NULL
+  std::optional<localNode> localNeighbour(const localNode& n, int d);
+  std::optional<localNode> maxRiskNode();
+  // the reference's public localNode::state written by a caller (its loop closes each
+  // popped node, L:654)
+  void setLocalNodeState(const localNode& n, node_state s);
+  void propagateRisk(const localNode& n);
+  void propagateLocalNode(const localNode& n);
+  std::optional<localNode> minCostLocalNode(double Tovertake, double minC);
+  std::optional<localNode> minCostLocalNode(const localNode& reachNode);
+  // the reference's public local lists (src/DyMu.hpp:448-454) as snapshots, in their
+  // order: local_narrowband (insertion order), local_expandable_obstacles (queue
+  // order), local_propagated_nodes (insertion order)
+  std::vector<localNode> localNarrowband();
+  std::vector<localNode> localExpandableObstacles();
+  std::vector<localNode> localPropagatedNodes();
   // L:441-471 against current_path
   bool isBlockingObstacle(const localNode& obNode, unsigned& maxIndex, unsigned& minIndex);
   // the reference's local_agent (src/DyMu.hpp:460): the last local propagation's
@@ -251,6 +295,17 @@ class DyMuPathPlanner {
   // the reference's node state: CLOSED iff popped by its FMM (finite T not above
   // the last early-exit limit; every finite cell after a full solve)
   bool closedCell(uint64_t k) const;
+  // node states written by a caller (setGlobalNodeState, resetTotalCostMap): empty =
+  // derived from the last solve (closedCell's rule), else 1 = CLOSED per node
+  std::vector<uint8_t> node_state_;
+  void materializeStates();
+  // nodes propagateGlobalNode made finite (global_propagated_nodes beyond the map's)
+  std::vector<uint64_t> propagated_extra_;
+  bool manual_list_ = false;  // after resetTotalCostMap: the list is propagated_extra_ alone
+  // local per-node helpers (csrc/local_layer.cpp)
+  void riskUpdate(uint64_t q);
+  void deviationUpdate(uint64_t q);
+  int64_t localId(const localNode& n) const;
   void markDirty(unsigned j0, unsigned j1);
   void ensureEngine();
   // pack F for the dirty rows, upload the rows whose speed changed; returns false

@@ -102,6 +102,15 @@ int dymu_planner_min_cost_global_node(dymu_planner* p, uint32_t* ij, double* tot
 int dymu_planner_reset_global_narrow_band(dymu_planner* p);                      /* :487-498 */
 /* gradientNode (:718-772): the normalised descent direction at (i, j) in d[2] */
 int dymu_planner_gradient_node(dymu_planner* p, uint32_t i, uint32_t j, double* d);
+/* propagateGlobalNode (:500-546): the reference update of node (i, j) from its
+ * nb4's current total costs on the host copy of the map; a node whose total cost
+ * was +inf joins the band (appended) and global_propagated_nodes */
+int dymu_planner_propagate_global_node(dymu_planner* p, uint32_t i, uint32_t j);
+/* the public globalNode::state (0 OPEN, 1 CLOSED) written by a caller */
+int dymu_planner_set_global_node_state(dymu_planner* p, uint32_t i, uint32_t j, int state);
+/* global_propagated_nodes (:447): the count; up to max (i, j) pairs in ij
+ * (DyMuPathPlanner::globalPropagatedNodes order) */
+int64_t dymu_planner_global_propagated_nodes(dymu_planner* p, uint32_t* ij, int64_t max);
 /* install a total-cost map (ny*nx, +inf unreachable) as a converged
  * computeEntireTotalCostMap leaves it (every finite node CLOSED) */
 int dymu_planner_load_total_cost_map(dymu_planner* p, const double* T);
@@ -146,6 +155,38 @@ int dymu_planner_get_reconnecting_index(dymu_planner* p);
 int dymu_planner_res_ratio(dymu_planner* p);
 /* subdivided global nodes: count, and a ny*nx byte mask (may be NULL) */
 int64_t dymu_planner_local_map_mask(dymu_planner* p, uint8_t* mask);
+/* a local-layer sub-cell (the reference's localNode, src/DyMu.hpp:42-67); id names
+ * it for the calls below (stable while the local map lives) */
+typedef struct dymu_local_node {
+  double global_x, global_y;  /* global_pose (global units) */
+  double deviation, total_cost, risk;
+  uint32_t parent_i, parent_j; /* the subdivided global node */
+  uint32_t li, lj;             /* the sub-cell inside it */
+  int32_t state, is_obstacle;  /* 0 OPEN / 1 CLOSED; 0 / 1 */
+  uint64_t id;
+} dymu_local_node;
+/* getLocalNode(Waypoint) (L:177-189; subdivides): 1 and *out, or 0 (NULL) */
+int dymu_planner_get_local_node(dymu_planner* p, double x, double y, dymu_local_node* out);
+/* localNode::nb4List[d] of sub-cell id (d: 0 (i,j-1), 1 (i-1,j), 2 (i+1,j),
+ * 3 (i,j+1)): 1 and *out, or 0 (NULL) */
+int dymu_planner_local_neighbour(dymu_planner* p, uint64_t id, int d, dymu_local_node* out);
+/* maxRiskNode (L:525-548): 1 and the popped node, or 0 (empty queue: NULL) */
+int dymu_planner_max_risk_node(dymu_planner* p, dymu_local_node* out);
+/* propagateRisk (L:550-576) / propagateLocalNode (L:700-750) on sub-cell id */
+int dymu_planner_propagate_risk(dymu_planner* p, uint64_t id);
+int dymu_planner_propagate_local_node(dymu_planner* p, uint64_t id);
+/* the public localNode::state (0 OPEN, 1 CLOSED) written by a caller */
+int dymu_planner_set_local_node_state(dymu_planner* p, uint64_t id, int state);
+/* minCostLocalNode(Tovertake, minC) (L:752-775) / minCostLocalNode(reachNode)
+ * (L:777-805): 1 and the popped band node, or 0 (empty band) */
+int dymu_planner_min_cost_local_node(dymu_planner* p, double Tovertake, double minC,
+                                     dymu_local_node* out);
+int dymu_planner_min_cost_local_node_reach(dymu_planner* p, uint64_t reach_id,
+                                           dymu_local_node* out);
+/* the public local lists (src/DyMu.hpp:448-454): which = 0 local_narrowband, 1
+ * local_expandable_obstacles, 2 local_propagated_nodes; the count, up to max
+ * written to out in the list's order */
+int64_t dymu_planner_local_list(dymu_planner* p, int which, dymu_local_node* out, int64_t max);
 /* one subdivided node's r*r sub-cells ([j][i]); 0 if (i, j) has no local map */
 int dymu_planner_local_block(dymu_planner* p, uint32_t i, uint32_t j, double* dev, double* tc,
                              double* risk, uint8_t* state, uint8_t* obst);

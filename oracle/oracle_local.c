@@ -959,3 +959,70 @@ int oracle_local_block(const oracle_local* L, uint32_t gi, uint32_t gj, double* 
   }
   return 1;
 }
+
+/* ---- the per-node steps and public lists (src/DyMu.hpp:448-454, :553-570) ----
+ * Test entry points for the product's class-surface per-node methods: a node is
+ * named by the position getLocalNode(Pose2D) resolves (L:160-173; subdivides, as
+ * the product's getLocalNode does); a node is reported as 5 doubles
+ * (global x, global y, deviation, total cost, risk). */
+static void node5(const lnode* n, double* out) {
+  out[0] = n->gpose[0];
+  out[1] = n->gpose[1];
+  out[2] = n->deviation;
+  out[3] = n->total_cost;
+  out[4] = n->risk;
+}
+
+/* which: 0 local_narrowband, 1 local_expandable_obstacles, 2 local_propagated_nodes */
+int oracle_local_list(const oracle_local* L, int which, double* out, int max) {
+  const pvec* v = which == 0 ? &L->narrow : which == 1 ? &L->expandable : &L->propagated;
+  for (size_t i = 0; i < v->n && (int)i < max; i++) node5(v->v[i], out + 5 * i);
+  return (int)v->n;
+}
+
+int oracle_local_max_risk_node(oracle_local* L, double* out) { /* L:525-548 */
+  lnode* n = max_risk_node(L);
+  if (!n) return 0;
+  node5(n, out);
+  return 1;
+}
+
+int oracle_local_propagate_risk_at(oracle_local* L, double x, double y) { /* L:550-576 */
+  lnode* n = get_local_node(L, x, y);
+  if (!n) return 0;
+  propagate_risk(L, n);
+  return 1;
+}
+
+int oracle_local_propagate_local_at(oracle_local* L, double x, double y) { /* L:700-750 */
+  lnode* n = get_local_node(L, x, y);
+  if (!n) return 0;
+  propagate_local(L, n);
+  return 1;
+}
+
+int oracle_local_set_state_at(oracle_local* L, double x, double y, int closed) {
+  lnode* n = get_local_node(L, x, y);
+  if (!n) return 0;
+  n->state = closed ? 1 : 0;
+  return 1;
+}
+
+/* L:752-775 / L:777-805; reach_x = NaN selects the SWEEPING key.  0 on an empty
+ * band (the reference reads front() of an empty vector: U3) */
+int oracle_local_min_cost(oracle_local* L, double reach_x, double reach_y, double* out) {
+  if (L->narrow.n == 0) return 0;
+  lnode* n;
+  if (reach_x != reach_x) {
+    n = min_cost_local(L);
+  } else {
+    lnode* r = get_local_node(L, reach_x, reach_y);
+    if (!r) return 0;
+    n = min_cost_local_reach(L, r);
+  }
+  node5(n, out);
+  return 1;
+}
+
+/* expandRisk (L:493-523) as a whole */
+void oracle_local_expand_risk(oracle_local* L) { expand_risk(L); }

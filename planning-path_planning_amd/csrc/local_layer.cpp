@@ -230,21 +230,49 @@ std::optional<localNode> DyMuPathPlanner::localAgent() {
 // reference's order: the front unless it is below 1 and a later entry has a
 // higher risk, in which case the first such entry; a node is queued again
 // each time its risk rises.
+namespace {
+// maxRiskNode's choice (:525-548): the front, unless it is below 1 and a later
+// entry holds a higher risk -- then the first such entry
+size_t max_risk_index(const LocalLayer& L) {
+  size_t index = 0;
+  double maxRisk = L.risk[L.expandable.front()];
+  for (size_t i = 0; i < L.expandable.size(); ++i) {
+    if (maxRisk == 1) break;
+    if (L.risk[L.expandable[i]] > maxRisk) {
+      maxRisk = L.risk[L.expandable[i]];
+      index = i;
+      break;
+    }
+  }
+  return index;
+}
+}  // namespace
+
+// propagateRisk (:550-576) on sub-cell q
+void DyMuPathPlanner::riskUpdate(uint64_t q) {
+  LocalLayer& L = *local_;
+  const double C = local_res_ / risk_distance_;
+  const int64_t y0 = L.nb(q, 0), y1 = L.nb(q, 3), x0 = L.nb(q, 1), x1 = L.nb(q, 2);
+  const double Ry = std::fmax(y0 < 0 ? 0 : L.risk[y0], y1 < 0 ? 0 : L.risk[y1]);
+  const double Rx = std::fmax(x0 < 0 ? 0 : L.risk[x0], x1 < 0 ? 0 : L.risk[x1]);
+  const double Sx = 1 - Rx, Sy = 1 - Ry;
+  double S;
+  if (std::fabs(Sx - Sy) < C)
+    S = (Sx + Sy + std::sqrt(2 * (C * C) - ((Sx - Sy) * (Sx - Sy)))) / 2;
+  else
+    S = std::fmin(Sx, Sy) + C;
+  const double R = (1 - S < 0.0) ? 0.0 : 1 - S;
+  if ((R > 0) && (R > L.risk[q])) {
+    L.risk[q] = R;
+    L.expandable.push_back(q);
+  }
+}
+
 void DyMuPathPlanner::expandRisk() {
   if (!local_) return;
   LocalLayer& L = *local_;
-  const double C = local_res_ / risk_distance_;
   while (!L.expandable.empty()) {
-    size_t index = 0;
-    double maxRisk = L.risk[L.expandable.front()];
-    for (size_t i = 0; i < L.expandable.size(); ++i) {
-      if (maxRisk == 1) break;
-      if (L.risk[L.expandable[i]] > maxRisk) {
-        maxRisk = L.risk[L.expandable[i]];
-        index = i;
-        break;
-      }
-    }
+    const size_t index = max_risk_index(L);
     const uint64_t t = L.expandable[index];
     L.expandable.erase(L.expandable.begin() + (std::ptrdiff_t)index);
     const CellPose ct = cell_pose(L, t, nx_, global_res_);
@@ -255,23 +283,127 @@ void DyMuPathPlanner::expandRisk() {
       const CellPose cq = cell_pose(L, (uint64_t)q, nx_, global_res_);
       const int64_t g = nearestIndex(cq.px, cq.py);
       if (gt != g && g >= 0) subdivideGlobalNode((unsigned)(g % nx_), (unsigned)(g / nx_));
-      // propagateRisk (:550-576)
-      const int64_t y0 = L.nb(q, 0), y1 = L.nb(q, 3), x0 = L.nb(q, 1), x1 = L.nb(q, 2);
-      const double Ry = std::fmax(y0 < 0 ? 0 : L.risk[y0], y1 < 0 ? 0 : L.risk[y1]);
-      const double Rx = std::fmax(x0 < 0 ? 0 : L.risk[x0], x1 < 0 ? 0 : L.risk[x1]);
-      const double Sx = 1 - Rx, Sy = 1 - Ry;
-      double S;
-      if (std::fabs(Sx - Sy) < C)
-        S = (Sx + Sy + std::sqrt(2 * (C * C) - ((Sx - Sy) * (Sx - Sy)))) / 2;
-      else
-        S = std::fmin(Sx, Sy) + C;
-      const double R = (1 - S < 0.0) ? 0.0 : 1 - S;
-      if ((R > 0) && (R > L.risk[q])) {
-        L.risk[q] = R;
-        L.expandable.push_back((uint64_t)q);
-      }
+      riskUpdate((uint64_t)q);
     }
   }
+}
+
+// ---- the per-node steps at the class surface (src/DyMu.hpp:553-570) ----
+
+int64_t DyMuPathPlanner::localId(const localNode& n) const {
+  if (!local_ || n.id >= local_->dev.size()) return -1;
+  return (int64_t)n.id;
+}
+
+std::optional<localNode> DyMuPathPlanner::localNeighbour(const localNode& n, int d) {
+  const int64_t p = localId(n);
+  if (p < 0 || d < 0 || d > 3) return std::nullopt;
+  const int64_t q = local_->nb((uint64_t)p, d);
+  if (q < 0) return std::nullopt;
+  localNode o;
+  localCell((uint64_t)q, &o);
+  return o;
+}
+
+std::optional<localNode> DyMuPathPlanner::maxRiskNode() {
+  if (!local_ || local_->expandable.empty()) return std::nullopt;  // :527
+  LocalLayer& L = *local_;
+  const size_t index = max_risk_index(L);
+  const uint64_t t = L.expandable[index];
+  L.expandable.erase(L.expandable.begin() + (std::ptrdiff_t)index);
+  localNode n;
+  localCell(t, &n);
+  return n;
+}
+
+void DyMuPathPlanner::propagateRisk(const localNode& n) {
+  const int64_t q = localId(n);
+  if (q >= 0) riskUpdate((uint64_t)q);
+}
+
+void DyMuPathPlanner::propagateLocalNode(const localNode& n) {
+  const int64_t q = localId(n);
+  if (q >= 0) deviationUpdate((uint64_t)q);
+}
+
+void DyMuPathPlanner::setLocalNodeState(const localNode& n, node_state s) {
+  const int64_t q = localId(n);
+  if (q >= 0) local_->state[q] = s == CLOSED ? 1 : 0;
+}
+
+// the band in the reference's order: a sub-cell enters local_narrowband exactly when
+// it enters local_propagated_nodes (its deviation first becomes finite, :741-747),
+// so the band is the propagated list filtered by membership
+std::optional<localNode> DyMuPathPlanner::minCostLocalNode(double Tovertake, double minC) {
+  (void)Tovertake;  // the reference's key ignores them (the term is commented out, :758)
+  (void)minC;
+  if (!local_) return std::nullopt;
+  LocalLayer& L = *local_;
+  int64_t best = -1;
+  for (const uint64_t p : L.propagated)
+    if (L.in_band[p] && (best < 0 || L.dev[p] < L.dev[best])) best = (int64_t)p;
+  if (best < 0) return std::nullopt;  // the reference reads front() of an empty band (U3)
+  L.in_band[best] = 0;
+  --L.band_count;
+  localNode n;
+  localCell((uint64_t)best, &n);
+  return n;
+}
+
+std::optional<localNode> DyMuPathPlanner::minCostLocalNode(const localNode& reachNode) {
+  const int64_t r = localId(reachNode);
+  if (r < 0) return std::nullopt;
+  LocalLayer& L = *local_;
+  const CellPose ce = cell_pose(L, (uint64_t)r, nx_, global_res_);
+  int64_t best = -1;
+  double hmin = 0.0;
+  for (const uint64_t p : L.propagated) {
+    if (!L.in_band[p]) continue;
+    const CellPose c = cell_pose(L, p, nx_, global_res_);
+    const double dx = c.wx - ce.wx, dy = c.wy - ce.wy;
+    const double h = L.dev[p] + std::sqrt(dx * dx + dy * dy);  // :782-800
+    if (best < 0 || h < hmin) {
+      hmin = h;
+      best = (int64_t)p;
+    }
+  }
+  if (best < 0) return std::nullopt;
+  L.in_band[best] = 0;
+  --L.band_count;
+  localNode n;
+  localCell((uint64_t)best, &n);
+  return n;
+}
+
+std::vector<localNode> DyMuPathPlanner::localNarrowband() {
+  std::vector<localNode> out;
+  if (!local_) return out;
+  for (const uint64_t p : local_->propagated) {
+    if (!local_->in_band[p]) continue;
+    out.emplace_back();
+    localCell(p, &out.back());
+  }
+  return out;
+}
+
+std::vector<localNode> DyMuPathPlanner::localExpandableObstacles() {
+  std::vector<localNode> out;
+  if (!local_) return out;
+  for (const uint64_t p : local_->expandable) {
+    out.emplace_back();
+    localCell(p, &out.back());
+  }
+  return out;
+}
+
+std::vector<localNode> DyMuPathPlanner::localPropagatedNodes() {
+  std::vector<localNode> out;
+  if (!local_) return out;
+  for (const uint64_t p : local_->propagated) {
+    out.emplace_back();
+    localCell(p, &out.back());
+  }
+  return out;
 }
 
 // :578-805 (computeLocalPropagation, propagateLocalNode, minCostLocalNode x2);
@@ -357,35 +489,9 @@ int64_t DyMuPathPlanner::localPropagation(base::Waypoint start, base::Waypoint o
       }
       q = L.nb((uint64_t)t, d);
       if (q < 0 || L.state[q] || L.obst[q]) continue;
-      // propagateLocalNode (:700-750)
-      const int64_t n0 = L.nb(q, 0), n3 = L.nb(q, 3), n1 = L.nb(q, 1), n2 = L.nb(q, 2);
-      double Ty, Tx;
-      if (n0 >= 0 && n3 >= 0)
-        Ty = std::fmin(L.dev[n3], L.dev[n0]);
-      else if (n0 < 0)
-        Ty = n3 >= 0 ? L.dev[n3] : kInf;
-      else
-        Ty = L.dev[n0];
-      if (n1 >= 0 && n2 >= 0)
-        Tx = std::fmin(L.dev[n1], L.dev[n2]);
-      else if (n1 < 0)
-        Tx = n2 >= 0 ? L.dev[n2] : kInf;
-      else
-        Tx = L.dev[n1];
-      const double R = L.risk[q];
-      if (L.tc[q] == kInf) L.tc[q] = localTotalCost((uint64_t)q);
-      const double C = local_res_ * (risk_ratio_ * R + 1);
-      const double Tn = eikonal(Tx, Ty, C);
-      if (Tn < L.dev[q]) {
-        if (L.dev[q] == kInf) {
-          L.seq[q] = L.next_seq++;
-          L.in_band[q] = 1;
-          ++L.band_count;
-          L.propagated.push_back((uint64_t)q);
-        }
-        L.dev[q] = Tn;
-        band_push((uint64_t)q);
-      }
+      const double d0 = L.dev[q];
+      deviationUpdate((uint64_t)q);  // propagateLocalNode (:700-750)
+      if (L.dev[q] < d0) band_push((uint64_t)q);
       if (end < 0 && L.tc[q] < Tover && L.risk[q] == 0) end = q;
     }
     if (end >= 0 && L.state[end]) {
@@ -406,6 +512,39 @@ int64_t DyMuPathPlanner::localPropagation(base::Waypoint start, base::Waypoint o
                    (unsigned long long)L.propagated.size());
       return -1;
     }
+  }
+}
+
+// propagateLocalNode (:700-750) on sub-cell q: the deviation update; a sub-cell whose
+// deviation first becomes finite joins the band and the propagated list
+void DyMuPathPlanner::deviationUpdate(uint64_t q) {
+  LocalLayer& L = *local_;
+  const int64_t n0 = L.nb(q, 0), n3 = L.nb(q, 3), n1 = L.nb(q, 1), n2 = L.nb(q, 2);
+  double Ty, Tx;
+  if (n0 >= 0 && n3 >= 0)
+    Ty = std::fmin(L.dev[n3], L.dev[n0]);
+  else if (n0 < 0)
+    Ty = n3 >= 0 ? L.dev[n3] : kInf;
+  else
+    Ty = L.dev[n0];
+  if (n1 >= 0 && n2 >= 0)
+    Tx = std::fmin(L.dev[n1], L.dev[n2]);
+  else if (n1 < 0)
+    Tx = n2 >= 0 ? L.dev[n2] : kInf;
+  else
+    Tx = L.dev[n1];
+  const double R = L.risk[q];
+  if (L.tc[q] == kInf) L.tc[q] = localTotalCost(q);
+  const double C = local_res_ * (risk_ratio_ * R + 1);
+  const double Tn = eikonal(Tx, Ty, C);
+  if (Tn < L.dev[q]) {
+    if (L.dev[q] == kInf) {
+      L.seq[q] = L.next_seq++;
+      L.in_band[q] = 1;
+      ++L.band_count;
+      L.propagated.push_back(q);
+    }
+    L.dev[q] = Tn;
   }
 }
 

@@ -113,6 +113,9 @@ bool DyMuPathPlanner::initGlobalLayer(double globalres, double localres, unsigne
   blk_missing_ = 0;
   closed_limit_ = 0.0;
   band_cells_.clear();
+  node_state_.clear();
+  propagated_extra_.clear();
+  manual_list_ = false;
   speed_.clear();
   speed_valid_ = false;
   markDirty(0, ny_);
@@ -639,6 +642,7 @@ void DyMuPathPlanner::copyTotalCost(double* out, bool raw) const {
 }
 
 bool DyMuPathPlanner::closedCell(uint64_t k) const {
+  if (!node_state_.empty()) return node_state_[k] != 0;
   const double t = T(k);
   return t < kInf && t <= closed_limit_;
 }
@@ -683,10 +687,13 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
                                dymu_last_error(ctx_));
     incremental_ = 0;
   }
-  // the host mirror is stale
+  // the host mirror is stale; node states and the propagated list follow the new map
   std::fill(blk_ok_.begin(), blk_ok_.end(), 0);
   blk_missing_ = blk_ok_.size();
   band_cells_.clear();
+  node_state_.clear();
+  propagated_extra_.clear();
+  manual_list_ = false;
   if (!early) {
     closed_limit_ = kInf;
     solved_ = true;
@@ -1104,14 +1111,102 @@ bool DyMuPathPlanner::isFullyClosedNode(unsigned i, unsigned j) {
          closedCell(k + nx_);
 }
 
-// :473-485
+// :473-485: every node OPEN at +inf, global_propagated_nodes cleared
 void DyMuPathPlanner::resetTotalCostMap() {
   std::fill(total_cost_.begin(), total_cost_.end(), kInf);
   std::fill(blk_ok_.begin(), blk_ok_.end(), 1);
   blk_missing_ = 0;
   closed_limit_ = 0.0;
   band_cells_.clear();
+  node_state_.assign(total_cost_.size(), 0);
+  propagated_extra_.clear();
+  manual_list_ = true;
   solved_ = false;
+}
+
+// the node states of the last solve made explicit, so a caller can change some
+void DyMuPathPlanner::materializeStates() {
+  if (!node_state_.empty()) return;
+  fetchAll();
+  std::vector<uint8_t> st(total_cost_.size());
+  for (uint64_t k = 0; k < st.size(); ++k) st[k] = closedCell(k) ? 1 : 0;
+  node_state_ = std::move(st);
+}
+
+void DyMuPathPlanner::setGlobalNodeState(unsigned i, unsigned j, node_state s) {
+  if (i >= nx_ || j >= ny_) return;
+  materializeStates();
+  node_state_[idx(i, j)] = s == CLOSED ? 1 : 0;
+}
+
+// :500-546, on the host copy of the map (made whole first, so no later download
+// of device blocks can overwrite what this writes)
+void DyMuPathPlanner::propagateGlobalNode(unsigned i, unsigned j) {
+  if (i >= nx_ || j >= ny_) return;
+  fetchAll();
+  const uint64_t k = idx(i, j);
+  const double* t = total_cost_.data();
+  const bool n0 = j > 0, n3 = j + 1 < ny_, n1 = i > 0, n2 = i + 1 < nx_;
+  // a NULL neighbour: the other one alone (:504-523); none at all (a 1-wide grid, a
+  // NULL dereference in the reference): +inf
+  double Ty, Tx;
+  if (n0 && n3)
+    Ty = std::fmin(t[k + nx_], t[k - nx_]);
+  else if (!n0)
+    Ty = n3 ? t[k + nx_] : kInf;
+  else
+    Ty = t[k - nx_];
+  if (n1 && n2)
+    Tx = std::fmin(t[k - 1], t[k + 1]);
+  else if (!n1)
+    Tx = n2 ? t[k + 1] : kInf;
+  else
+    Tx = t[k - 1];
+  const double C = global_res_ * (cost_[k]) * (2 + hazard_[k] - traff_[k]);  // :527-528
+  double Tn;
+  if ((std::fabs(Tx - Ty) < C) && (Tx < kInf) && (Ty < kInf))
+    Tn = (Tx + Ty + std::sqrt(2 * (C * C) - ((Tx - Ty) * (Tx - Ty)))) / 2;  // pow(., 2.0) == x*x
+  else
+    Tn = std::fmin(Tx, Ty) + C;
+  if (Tn < total_cost_[k]) {
+    if (total_cost_[k] == kInf) {
+      propagated_extra_.push_back(k);
+      band_cells_.push_back(k);  // insertion order, as the reference's vector
+    }
+    total_cost_[k] = Tn;
+    solved_ = false;  // the device map no longer matches the host's
+  }
+}
+
+void DyMuPathPlanner::propagateGlobalNode(const globalNode& n) {
+  propagateGlobalNode(grid_u32(n.pose.position[0]), grid_u32(n.pose.position[1]));
+}
+
+uint64_t DyMuPathPlanner::globalPropagatedCount() {
+  if (manual_list_) return propagated_extra_.size();
+  uint64_t c = propagated_extra_.size();
+  streamTotalCost([&](unsigned r0, unsigned r1) {
+    const double* t = total_cost_.data();
+    for (uint64_t k = idx(0, r0); k < idx(0, r1); ++k) c += t[k] < kInf ? 1 : 0;
+  });
+  // nodes propagateGlobalNode made finite are counted in the map already
+  return c - propagated_extra_.size();
+}
+
+std::vector<globalNode> DyMuPathPlanner::globalPropagatedNodes() {
+  std::vector<globalNode> out;
+  if (!manual_list_) {
+    fetchAll();
+    std::vector<uint8_t> extra;
+    if (!propagated_extra_.empty()) {
+      extra.assign(total_cost_.size(), 0);
+      for (const uint64_t k : propagated_extra_) extra[k] = 1;
+    }
+    for (uint64_t k = 0; k < total_cost_.size(); ++k)
+      if (total_cost_[k] < kInf && (extra.empty() || !extra[k])) out.push_back(*snapshot(k));
+  }
+  for (const uint64_t k : propagated_extra_) out.push_back(*snapshot(k));
+  return out;
 }
 
 std::vector<globalNode> DyMuPathPlanner::globalNarrowband() {
@@ -1146,6 +1241,7 @@ void DyMuPathPlanner::resetGlobalNarrowBand() {
   (void)T(k);  // the goal's block in the host mirror before the write
   total_cost_[k] = 0.0;
   band_cells_.push_back(k);
+  propagated_extra_.push_back(k);  // global_propagated_nodes.push_back(global_goal)
 }
 
 bool DyMuPathPlanner::loadTotalCostMap(const double* Tin) {
@@ -1156,6 +1252,9 @@ bool DyMuPathPlanner::loadTotalCostMap(const double* Tin) {
   blk_missing_ = 0;
   closed_limit_ = kInf;
   band_cells_.clear();
+  node_state_.clear();
+  propagated_extra_.clear();
+  manual_list_ = false;
   solved_ = false;
   if (ctx_ && dT_ && dcells_ == n &&
       dymu_memcpy_h2d(ctx_, dT_, total_cost_.data(), sizeof(double) * n) != DYMU_OK)

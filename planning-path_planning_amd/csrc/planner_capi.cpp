@@ -12,6 +12,9 @@
 #include "dymu_planner.h"
 
 using PathPlanning_lib::DyMuPathPlanner;
+using PathPlanning_lib::localNode;
+using PathPlanning_lib::CLOSED;
+using PathPlanning_lib::OPEN;
 
 struct dymu_planner {
   DyMuPathPlanner pl;
@@ -293,6 +296,43 @@ int dymu_planner_gradient_node(dymu_planner* p, uint32_t i, uint32_t j, double* 
   });
 }
 
+int dymu_planner_propagate_global_node(dymu_planner* p, uint32_t i, uint32_t j) {
+  if (!p) return DYMU_ERR_ARG;
+  return guarded([&] {
+    if (i >= p->pl.sizeX() || j >= p->pl.sizeY()) return (int)DYMU_ERR_ARG;
+    p->pl.propagateGlobalNode(i, j);
+    return (int)DYMU_OK;
+  });
+}
+
+int dymu_planner_set_global_node_state(dymu_planner* p, uint32_t i, uint32_t j, int state) {
+  if (!p || (state != 0 && state != 1)) return DYMU_ERR_ARG;
+  return guarded([&] {
+    if (i >= p->pl.sizeX() || j >= p->pl.sizeY()) return (int)DYMU_ERR_ARG;
+    p->pl.setGlobalNodeState(i, j, state ? CLOSED : OPEN);
+    return (int)DYMU_OK;
+  });
+}
+
+int64_t dymu_planner_global_propagated_nodes(dymu_planner* p, uint32_t* ij, int64_t max) {
+  if (!p || (max > 0 && !ij)) return DYMU_ERR_ARG;
+  int64_t n = 0;
+  const int rc = guarded([&] {
+    if (max <= 0) {
+      n = (int64_t)p->pl.globalPropagatedCount();
+      return DYMU_OK;
+    }
+    const auto nodes = p->pl.globalPropagatedNodes();
+    n = (int64_t)nodes.size();
+    for (int64_t q = 0; q < n && q < max; ++q) {
+      ij[2 * q] = (uint32_t)nodes[q].pose.position[0];
+      ij[2 * q + 1] = (uint32_t)nodes[q].pose.position[1];
+    }
+    return DYMU_OK;
+  });
+  return rc < 0 ? rc : n;
+}
+
 int dymu_planner_reset_total_cost_map(dymu_planner* p) {
   if (!p) return DYMU_ERR_ARG;
   p->pl.resetTotalCostMap();
@@ -406,6 +446,112 @@ int dymu_planner_local_agent(dymu_planner* p, double* xy) {
     xy[1] = n->global_pose.position[1];
     return 1;
   });
+}
+
+namespace {
+void flat_local(const localNode& n, dymu_local_node* out) {
+  out->global_x = n.global_pose.position[0];
+  out->global_y = n.global_pose.position[1];
+  out->deviation = n.deviation;
+  out->total_cost = n.total_cost;
+  out->risk = n.risk;
+  out->parent_i = (uint32_t)n.parent_pose.position[0];
+  out->parent_j = (uint32_t)n.parent_pose.position[1];
+  out->li = (uint32_t)n.pose.position[0];
+  out->lj = (uint32_t)n.pose.position[1];
+  out->state = n.state == CLOSED ? 1 : 0;
+  out->is_obstacle = n.isObstacle ? 1 : 0;
+  out->id = n.id;
+}
+localNode by_id(uint64_t id) {
+  localNode n;
+  n.id = id;
+  return n;
+}
+}  // namespace
+
+int dymu_planner_get_local_node(dymu_planner* p, double x, double y, dymu_local_node* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  return guarded([&] {
+    const auto n = p->pl.getLocalNode(wp(x, y, 0.0, 0.0));
+    if (!n) return 0;
+    flat_local(*n, out);
+    return 1;
+  });
+}
+
+int dymu_planner_local_neighbour(dymu_planner* p, uint64_t id, int d, dymu_local_node* out) {
+  if (!p || !out || d < 0 || d > 3) return DYMU_ERR_ARG;
+  return guarded([&] {
+    const auto n = p->pl.localNeighbour(by_id(id), d);
+    if (!n) return 0;
+    flat_local(*n, out);
+    return 1;
+  });
+}
+
+int dymu_planner_max_risk_node(dymu_planner* p, dymu_local_node* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  return guarded([&] {
+    const auto n = p->pl.maxRiskNode();
+    if (!n) return 0;
+    flat_local(*n, out);
+    return 1;
+  });
+}
+
+int dymu_planner_propagate_risk(dymu_planner* p, uint64_t id) {
+  if (!p) return DYMU_ERR_ARG;
+  return guarded([&] { p->pl.propagateRisk(by_id(id)); return (int)DYMU_OK; });
+}
+
+int dymu_planner_propagate_local_node(dymu_planner* p, uint64_t id) {
+  if (!p) return DYMU_ERR_ARG;
+  return guarded([&] { p->pl.propagateLocalNode(by_id(id)); return (int)DYMU_OK; });
+}
+
+int dymu_planner_set_local_node_state(dymu_planner* p, uint64_t id, int state) {
+  if (!p || (state != 0 && state != 1)) return DYMU_ERR_ARG;
+  return guarded([&] {
+    p->pl.setLocalNodeState(by_id(id), state ? CLOSED : OPEN);
+    return (int)DYMU_OK;
+  });
+}
+
+int dymu_planner_min_cost_local_node(dymu_planner* p, double Tovertake, double minC,
+                                     dymu_local_node* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  return guarded([&] {
+    const auto n = p->pl.minCostLocalNode(Tovertake, minC);
+    if (!n) return 0;
+    flat_local(*n, out);
+    return 1;
+  });
+}
+
+int dymu_planner_min_cost_local_node_reach(dymu_planner* p, uint64_t reach_id,
+                                           dymu_local_node* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  return guarded([&] {
+    const auto n = p->pl.minCostLocalNode(by_id(reach_id));
+    if (!n) return 0;
+    flat_local(*n, out);
+    return 1;
+  });
+}
+
+int64_t dymu_planner_local_list(dymu_planner* p, int which, dymu_local_node* out, int64_t max) {
+  if (!p || which < 0 || which > 2 || (max > 0 && !out)) return DYMU_ERR_ARG;
+  int64_t n = 0;
+  const int rc = guarded([&] {
+    const auto v = which == 0   ? p->pl.localNarrowband()
+                   : which == 1 ? p->pl.localExpandableObstacles()
+                                : p->pl.localPropagatedNodes();
+    n = (int64_t)v.size();
+    for (int64_t q = 0; q < n && q < max; ++q) flat_local(v[q], &out[q]);
+    return DYMU_OK;
+  });
+  return rc < 0 ? rc : n;
 }
 
 int dymu_planner_compute_local_propagation(dymu_planner* p, const double* s, const double* o,

@@ -490,6 +490,18 @@ PLANNER_SYMBOLS = {
     "dymu_planner_res_ratio": (_i32, [_vp]),
     "dymu_planner_local_map_mask": (ctypes.c_int64, [_vp, _vp]),
     "dymu_planner_local_block": (_i32, [_vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "dymu_planner_propagate_global_node": (_i32, [_vp, _u32, _u32]),
+    "dymu_planner_set_global_node_state": (_i32, [_vp, _u32, _u32, _i32]),
+    "dymu_planner_global_propagated_nodes": (ctypes.c_int64, [_vp, _vp, ctypes.c_int64]),
+    "dymu_planner_get_local_node": (_i32, [_vp, _d, _d, _vp]),
+    "dymu_planner_max_risk_node": (_i32, [_vp, _vp]),
+    "dymu_planner_local_neighbour": (_i32, [_vp, _u64, _i32, _vp]),
+    "dymu_planner_propagate_risk": (_i32, [_vp, _u64]),
+    "dymu_planner_propagate_local_node": (_i32, [_vp, _u64]),
+    "dymu_planner_set_local_node_state": (_i32, [_vp, _u64, _i32]),
+    "dymu_planner_min_cost_local_node": (_i32, [_vp, _d, _d, _vp]),
+    "dymu_planner_min_cost_local_node_reach": (_i32, [_vp, _u64, _vp]),
+    "dymu_planner_local_list": (ctypes.c_int64, [_vp, _i32, _vp, ctypes.c_int64]),
 }
 
 
@@ -498,6 +510,15 @@ class DymuGlobalNode(ctypes.Structure):
                 ("hazard_density", _d), ("trafficability", _d), ("total_cost", _d),
                 ("terrain", _u32), ("state", _i32), ("is_obstacle", _i32),
                 ("has_local_map", _i32)]
+
+class DymuLocalNode(ctypes.Structure):
+    _fields_ = [("global_x", _d), ("global_y", _d), ("deviation", _d), ("total_cost", _d),
+                ("risk", _d), ("parent_i", _u32), ("parent_j", _u32), ("li", _u32),
+                ("lj", _u32), ("state", _i32), ("is_obstacle", _i32), ("id", _u64)]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
 
 _pl = None
 
@@ -706,6 +727,80 @@ class Planner:
 
     def resetGlobalNarrowBand(self):
         _check(self._lib.dymu_planner_reset_global_narrow_band(self.h))
+
+    def propagateGlobalNode(self, i: int, j: int):
+        """propagateGlobalNode (:500-546) on node (i, j) (host copy of the map)."""
+        _check(self._lib.dymu_planner_propagate_global_node(self.h, i, j))
+
+    def setGlobalNodeState(self, i: int, j: int, closed: bool):
+        """The public globalNode::state: CLOSED (True) or OPEN."""
+        _check(self._lib.dymu_planner_set_global_node_state(self.h, i, j, 1 if closed else 0))
+
+    def globalPropagatedNodes(self) -> np.ndarray:
+        """global_propagated_nodes (:447): (n, 2) array of (i, j)."""
+        n = self._lib.dymu_planner_global_propagated_nodes(self.h, None, 0)
+        if n < 0:
+            _check(int(n))
+        ij = np.zeros((max(n, 1), 2), dtype=np.uint32)
+        m = self._lib.dymu_planner_global_propagated_nodes(self.h, ij.ctypes.data, n)
+        if m < 0:
+            _check(int(m))
+        return ij[:min(n, m)]
+
+    # the local layer's per-node steps (L:525-805); nodes are dicts with an "id"
+    def _local(self, fn, *args):
+        n = DymuLocalNode()
+        if not _b(fn(self.h, *args, ctypes.byref(n))):
+            return None
+        return n.as_dict()
+
+    def getLocalNode(self, x: float, y: float):
+        """getLocalNode(Waypoint) (L:177-189; subdivides): dict or None."""
+        return self._local(self._lib.dymu_planner_get_local_node, float(x), float(y))
+
+    def localNeighbour(self, node, d: int):
+        """node's nb4List[d] (0 (i,j-1), 1 (i-1,j), 2 (i+1,j), 3 (i,j+1)), or None."""
+        return self._local(self._lib.dymu_planner_local_neighbour, int(node["id"]), int(d))
+
+    def maxRiskNode(self):
+        return self._local(self._lib.dymu_planner_max_risk_node)
+
+    def propagateRisk(self, node):
+        _check(self._lib.dymu_planner_propagate_risk(self.h, int(node["id"])))
+
+    def propagateLocalNode(self, node):
+        _check(self._lib.dymu_planner_propagate_local_node(self.h, int(node["id"])))
+
+    def setLocalNodeState(self, node, closed: bool):
+        _check(self._lib.dymu_planner_set_local_node_state(self.h, int(node["id"]),
+                                                           1 if closed else 0))
+
+    def minCostLocalNode(self, Tovertake=None, minC=None, reach=None):
+        """minCostLocalNode(Tovertake, minC) (SWEEPING key) or minCostLocalNode(reach)
+        (CONSERVATIVE key: deviation + distance to reach)."""
+        if reach is not None:
+            return self._local(self._lib.dymu_planner_min_cost_local_node_reach, int(reach["id"]))
+        return self._local(self._lib.dymu_planner_min_cost_local_node, float(Tovertake or 0.0),
+                           float(minC or 0.0))
+
+    def _local_list(self, which: int) -> list:
+        n = self._lib.dymu_planner_local_list(self.h, which, None, 0)
+        if n < 0:
+            _check(int(n))
+        arr = (DymuLocalNode * max(n, 1))()
+        m = self._lib.dymu_planner_local_list(self.h, which, arr, n)
+        if m < 0:
+            _check(int(m))
+        return [arr[q].as_dict() for q in range(min(n, m))]
+
+    def localNarrowband(self) -> list:
+        return self._local_list(0)
+
+    def localExpandableObstacles(self) -> list:
+        return self._local_list(1)
+
+    def localPropagatedNodes(self) -> list:
+        return self._local_list(2)
 
     def gradientNode(self, i: int, j: int):
         """gradientNode (:718-772): (dnx, dny)."""

@@ -55,6 +55,13 @@ _SIGS = {
     "oracle_local_deviation_matrix": (None, [_vp, _d, _d, _vp]),
     "oracle_local_map_mask": (_u64, [_vp, _vp]),
     "oracle_local_block": (ctypes.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "oracle_local_list": (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int]),
+    "oracle_local_max_risk_node": (ctypes.c_int, [_vp, _vp]),
+    "oracle_local_propagate_risk_at": (ctypes.c_int, [_vp, _d, _d]),
+    "oracle_local_propagate_local_at": (ctypes.c_int, [_vp, _d, _d]),
+    "oracle_local_set_state_at": (ctypes.c_int, [_vp, _d, _d, ctypes.c_int]),
+    "oracle_local_min_cost": (ctypes.c_int, [_vp, _d, _d, _vp]),
+    "oracle_local_expand_risk": (None, [_vp]),
 }
 
 
@@ -151,6 +158,35 @@ class OracleLocal:
         m = np.zeros((self.ny, self.nx), dtype=np.uint8)
         self.lib.oracle_local_map_mask(self.h, m.ctypes.data)
         return m
+
+    # per-node steps and the public lists (5 doubles per node: global x, global y,
+    # deviation, total cost, risk)
+    def node_list(self, which):
+        n = self.lib.oracle_local_list(self.h, which, None, 0)
+        out = np.empty((max(n, 1), 5))
+        self.lib.oracle_local_list(self.h, which, out.ctypes.data, n)
+        return out[:n]
+
+    def max_risk_node(self):
+        out = np.empty(5)
+        return out if self.lib.oracle_local_max_risk_node(self.h, out.ctypes.data) else None
+
+    def propagate_risk(self, x, y):
+        return bool(self.lib.oracle_local_propagate_risk_at(self.h, x, y))
+
+    def propagate_local(self, x, y):
+        return bool(self.lib.oracle_local_propagate_local_at(self.h, x, y))
+
+    def set_state(self, x, y, closed):
+        return bool(self.lib.oracle_local_set_state_at(self.h, x, y, 1 if closed else 0))
+
+    def min_cost(self, reach=None):
+        out = np.empty(5)
+        rx, ry = reach if reach is not None else (float("nan"), 0.0)
+        return out if self.lib.oracle_local_min_cost(self.h, rx, ry, out.ctypes.data) else None
+
+    def expand_risk(self):
+        self.lib.oracle_local_expand_risk(self.h)
 
     def block(self, i, j):
         r = self.r

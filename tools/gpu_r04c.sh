@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 4: what a sparse pass costs -- grid barriers among few workgroups (one XCD vs
+# spread) against the launch, and the phase trace of one serpentine-maze pass.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r04c; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 120 ./tools/barrier_probe3 4000 > $O/barrier_probe3.log 2>&1 || { cat $O/barrier_probe3.log; exit 1; }
+cat $O/barrier_probe3.log
+DYMU_PRIO_TRACE=3000 timeout -k 10 300 python tools/maze_bench.py 4096 64 1 > $O/maze4096.json 2> $O/maze_trace.log || { tail $O/maze_trace.log; exit 1; }
+python tools/trace_show.py $O/maze_trace.log
+DYMU_PRIO_TRACE=1000 timeout -k 10 300 python tools/maze_bench.py 4096 64 1 > $O/maze4096b.json 2> $O/maze_trace_b.log || { tail $O/maze_trace_b.log; exit 1; }
+python tools/trace_show.py $O/maze_trace_b.log
