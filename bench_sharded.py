@@ -157,7 +157,7 @@ def run(args):
         # (DESIGN.md s5); every rank runs every candidate (transport x K, or the given K),
         # the max over ranks of the best of two solves decides, and all ranks get the
         # same choice.  Every candidate solve is a full solve of the same grid.
-        k_tune = {}
+        k_tune, sums = {}, {}
         ks = [args.passes_per_exchange] if args.passes_per_exchange else list(K_CANDIDATES)
         for tr in solvers:
             k_tune[tr] = {}
@@ -173,6 +173,16 @@ def run(args):
                     dist.all_reduce(el, op=dist.ReduceOp.MAX)
                     best = min(best, float(el.item()))
                 k_tune[tr][k] = round(best * 1e3, 3)
+            sums[tr] = _map_checksum(T_buf, nrows)
+        # a candidate whose map disagrees with the first candidate's (finite-cell count, or
+        # the sum beyond the tolerance) is dropped before the timed region; the timed
+        # transport's own map is checked in full afterwards (self_check)
+        first = next(iter(sums))
+        for tr in list(k_tune)[1:]:
+            (s0, n0), (s1, n1) = sums[first], sums[tr]
+            if n1 != n0 or abs(s1 - s0) > RTOL * max(abs(s0), 1.0):
+                dropped[tr] = f"map differs from {first}'s: sum {s1!r} vs {s0!r}, cells {n1} vs {n0}"
+                k_tune.pop(tr)
         # identical on every rank (max-reduced times)
         transport, K = min(((tr, k) for tr in k_tune for k in k_tune[tr]),
                            key=lambda c: k_tune[c[0]][c[1]])
@@ -233,6 +243,15 @@ def run(args):
     if rank != 0:
         return None
     return float(dt.item()), tot, kern_ms, kern_n, st
+
+
+def _map_checksum(T_buf, nrows):
+    """(sum, count) of the finite owned total costs over all ranks (gloo all-reduce)"""
+    own = T_buf[1:nrows + 1]
+    fin = torch.isfinite(own)
+    t = torch.tensor([float(own[fin].sum().item()), float(fin.sum().item())], dtype=torch.float64)
+    dist.all_reduce(t)
+    return float(t[0]), int(t[1])
 
 
 def _all_ok(ok):
