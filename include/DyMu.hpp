@@ -314,7 +314,10 @@ class DyMuPathPlanner {
   template <class ERows, class TRows>
   bool costMapFromRows(const ERows& elev_row, const TRows& terr_row);
   bool propagate(bool early, unsigned si, unsigned sj);
-  void replayBand(double t_closed, const std::vector<uint64_t>& band, std::vector<double>& out);
+  // returns true when the replay met equal values whose pop order decides the result
+  bool replayBand(double t_closed, const std::vector<uint64_t>& band, std::vector<double>& out);
+  // the reference's early exit replayed exactly on the host (ties at the exit)
+  bool exactEarlyExit(unsigned si, unsigned sj);
   bool safeNode(unsigned i, unsigned j) const;
   std::optional<globalNode> snapshot(uint64_t k);
   void nominalCost(unsigned i, unsigned j, int range, int num_locs, double cmax);

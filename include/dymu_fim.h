@@ -131,6 +131,12 @@ int dymu_solve_until_device(dymu_ctx* ctx, const double* dF, double* dT, uint32_
 int dymu_early_exit_mask(dymu_ctx* ctx, const double* dF, double* dT, uint32_t nx, uint32_t ny,
                          uint64_t ld, double t_closed, uint64_t* band_idx, uint64_t cap,
                          uint64_t* n_band, void* stream);
+/* *count = the number of cells of dT whose value is bitwise `value` (the early
+ * exit's tie test: cells of exactly t_closed other than the last one the
+ * reference closes make its CLOSED set depend on its insertion order).
+ * Synchronises `stream`. */
+int dymu_count_equal(dymu_ctx* ctx, const double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
+                     double value, uint64_t* count, void* stream);
 /* dT[(idx[k] / nx) * ld + idx[k] % nx] = vals[k] for k < n (idx, vals: host). */
 int dymu_scatter(dymu_ctx* ctx, double* dT, uint32_t nx, uint64_t ld, const uint64_t* idx,
                  const double* vals, uint64_t n, void* stream);

@@ -1262,6 +1262,20 @@ int dymu_early_exit_mask(dymu_ctx* c, const double* dF, double* dT, uint32_t nx,
   return DYMU_OK;
 }
 
+int dymu_count_equal(dymu_ctx* c, const double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
+                     double value, uint64_t* count, void* stream) {
+  if (!c || !dT || !count || ld < nx) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  hipStream_t st = pick_stream(c, stream);
+  unsigned long long* cnt = c->d_scratch + 4;
+  HIPC(c, hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
+  HIPC(c, launch_count_equal(dT, (int64_t)ld, nx, ny, value, cnt, st));
+  HIPC(c, hipMemcpyAsync(c->h_probe, cnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  HIPC(c, hipStreamSynchronize(st));
+  *count = c->h_probe[0];
+  return DYMU_OK;
+}
+
 int dymu_scatter(dymu_ctx* c, double* dT, uint32_t nx, uint64_t ld, const uint64_t* idx,
                  const double* vals, uint64_t n, void* stream) {
   if (!c || !dT || nx == 0 || ld < nx || (n && (!idx || !vals))) return DYMU_ERR_ARG;

@@ -718,9 +718,17 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
   }
   band.resize(nb);
   std::sort(band.begin(), band.end());
+  // exact ties decide the reference's CLOSED set (cells of exactly t_closed besides the
+  // last one it closes) or a band value (the replay met equal values): replay the
+  // reference exactly on the host instead
+  uint64_t at_t = 0;
+  if (t_closed < kInf &&
+      dymu_count_equal(ctx_, dT_, nx_, ny_, nx_, t_closed, &at_t, nullptr) != DYMU_OK)
+    throw std::runtime_error(std::string("dymu_count_equal failed: ") + dymu_last_error(ctx_));
+  if (at_t > 1) return exactEarlyExit(si, sj);
   if (nb) {
     std::vector<double> vals;
-    replayBand(t_closed, band, vals);
+    if (replayBand(t_closed, band, vals)) return exactEarlyExit(si, sj);
     rc = dymu_scatter(ctx_, dT_, nx_, nx_, band.data(), vals.data(), nb, nullptr);
     if (rc != DYMU_OK)
       throw std::runtime_error(std::string("dymu_scatter failed: ") + dymu_last_error(ctx_));
@@ -744,7 +752,7 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
 // takes that side and recursion only follows axes whose both sides are OPEN --
 // cells next to the front, at strictly earlier pops.  Ties between equal T
 // values (the reference's insertion order) are not reproduced.
-void DyMuPathPlanner::replayBand(double t_closed, const std::vector<uint64_t>& band,
+bool DyMuPathPlanner::replayBand(double t_closed, const std::vector<uint64_t>& band,
                                  std::vector<double>& out) {
   struct KeyHash {
     size_t operator()(const std::pair<uint64_t, double>& k) const {
@@ -759,12 +767,19 @@ void DyMuPathPlanner::replayBand(double t_closed, const std::vector<uint64_t>& b
     double t_closed;
     int64_t NX, NY;
     std::unordered_map<std::pair<uint64_t, double>, double, KeyHash> memo;
+    // the popped cell whose update is being replayed, and whether a cell of exactly
+    // its value was met: then the reference's insertion order (which of the equal
+    // cells it popped first) decides the value, and the caller replays exactly
+    int64_t cur = -1;
+    bool tie = false;
 
     bool in_grid(int64_t i, int64_t j) const { return i >= 0 && j >= 0 && i < NX && j < NY; }
     // value of a cell CLOSED at (pop) time te, else +inf
-    double closed_val(int64_t i, int64_t j, double te) const {
+    double closed_val(int64_t i, int64_t j, double te) {
       if (!in_grid(i, j)) return kInf;
-      const double t = pl.T((uint64_t)j * NX + i);
+      const int64_t k = j * NX + i;
+      const double t = pl.T((uint64_t)k);
+      if (t == te && t <= t_closed && k != cur) tie = true;
       return (t <= t_closed && t <= te) ? t : kInf;
     }
     // the reference update (:504-535), -ffp-contract=off
@@ -794,10 +809,16 @@ void DyMuPathPlanner::replayBand(double t_closed, const std::vector<uint64_t>& b
       double v = kInf;
       const int64_t nb[4][2] = {{i, j - 1}, {i - 1, j}, {i + 1, j}, {i, j + 1}};
       for (const auto& e : nb) {
+        const int64_t saved = cur;
+        cur = in_grid(e[0], e[1]) ? e[1] * NX + e[0] : -1;
         const double te = closed_val(e[0], e[1], t);
-        if (!(te < kInf)) continue;  // not CLOSED by time t: no pop of it updated x yet
+        if (!(te < kInf)) {  // not CLOSED by time t: no pop of it updated x yet
+          cur = saved;
+          continue;
+        }
         const double tx = axis(i - 1, j, i + 1, j, te, depth);
         const double ty = axis(i, j - 1, i, j + 1, te, depth);
+        cur = saved;
         v = std::fmin(v, eikonal(tx, ty, C));
       }
       memo[key] = v;
@@ -806,6 +827,96 @@ void DyMuPathPlanner::replayBand(double t_closed, const std::vector<uint64_t>& b
   } rec{*this, speed_.data(), t_closed, (int64_t)nx_, (int64_t)ny_, {}};
   out.resize(band.size());
   for (size_t q = 0; q < band.size(); ++q) out[q] = rec.val(band[q], t_closed, 0);
+  return rec.tie;
+}
+
+// computeTotalCostMap (:364-408) replayed exactly on the host: the reference FMM with
+// its band as a heap keyed (T, first-insertion sequence) -- the pops of the
+// first-strict-minimum scan (:551-568) in the same order -- until the start and its
+// nb4 are CLOSED.  Used when the GPU's early exit met equal total costs whose order
+// decides the CLOSED set or a band value (constant-speed maps: every distance ties):
+// O(m log m) for the m cells the reference reaches.  The map, the node states, the
+// band (insertion order) and global_propagated_nodes become the reference's.
+bool DyMuPathPlanner::exactEarlyExit(unsigned si, unsigned sj) {
+  const uint64_t n = (uint64_t)nx_ * ny_;
+  const double* F = speed_.data();
+  std::vector<double> T(n, kInf);
+  std::vector<uint8_t> closed(n, 0);
+  std::vector<uint64_t> order;  // cells in the order they first became finite
+  struct E {
+    double t;
+    uint64_t seq, k;
+  };
+  auto later = [](const E& a, const E& b) { return a.t > b.t || (a.t == b.t && a.seq > b.seq); };
+  std::vector<E> heap;
+  std::vector<uint64_t> first(n, 0);
+  std::vector<uint8_t> in_band(n, 0);
+  const uint64_t g = idx(goal_i_, goal_j_), s = idx(si, sj);
+  T[g] = 0.0;
+  first[g] = 0;
+  order.push_back(g);
+  in_band[g] = 1;
+  heap.push_back({0.0, 0, g});
+  uint64_t band = 1;
+  auto fully_closed = [&] {  // :424-436 (the start is interior: safeNode)
+    return closed[s] && closed[s - nx_] && closed[s - 1] && closed[s + 1] && closed[s + nx_];
+  };
+  while (band > 0 && !fully_closed()) {
+    std::pop_heap(heap.begin(), heap.end(), later);
+    const E e = heap.back();
+    heap.pop_back();
+    if (!in_band[e.k] || e.t != T[e.k]) continue;  // a superseded entry
+    in_band[e.k] = 0;
+    --band;
+    closed[e.k] = 1;
+    const unsigned i = (unsigned)(e.k % nx_), j = (unsigned)(e.k / nx_);
+    const int64_t nb[4][2] = {{i, (int64_t)j - 1}, {(int64_t)i - 1, j}, {i + 1, j}, {i, j + 1}};
+    for (const auto& q : nb) {
+      if (q[0] < 0 || q[1] < 0 || q[0] >= nx_ || q[1] >= ny_) continue;
+      const uint64_t k = idx((unsigned)q[0], (unsigned)q[1]);
+      if (closed[k] || !(F[k] < kInf)) continue;
+      // propagateGlobalNode (:500-546) from the current values
+      const unsigned a = (unsigned)q[0], b = (unsigned)q[1];
+      const double Ty = (b > 0 && b + 1 < ny_) ? std::fmin(T[k + nx_], T[k - nx_])
+                        : b == 0              ? (b + 1 < ny_ ? T[k + nx_] : kInf)
+                                              : T[k - nx_];
+      const double Tx = (a > 0 && a + 1 < nx_) ? std::fmin(T[k - 1], T[k + 1])
+                        : a == 0              ? (a + 1 < nx_ ? T[k + 1] : kInf)
+                                              : T[k - 1];
+      const double C = F[k];
+      double u;
+      if ((std::fabs(Tx - Ty) < C) && (Tx < kInf) && (Ty < kInf))
+        u = (Tx + Ty + std::sqrt(2 * (C * C) - ((Tx - Ty) * (Tx - Ty)))) / 2;
+      else
+        u = std::fmin(Tx, Ty) + C;
+      if (u < T[k]) {
+        if (T[k] == kInf) {
+          first[k] = order.size();
+          order.push_back(k);
+          in_band[k] = 1;
+          ++band;
+        }
+        T[k] = u;
+        heap.push_back({u, first[k], k});
+        std::push_heap(heap.begin(), heap.end(), later);
+      }
+    }
+  }
+  // install: host mirror (whole), device map, states, band and propagated list
+  total_cost_.swap(T);
+  std::fill(blk_ok_.begin(), blk_ok_.end(), 1);
+  blk_missing_ = 0;
+  if (dymu_memcpy_h2d(ctx_, dT_, total_cost_.data(), sizeof(double) * n) != DYMU_OK)
+    throw std::runtime_error(std::string("dymu: total-cost upload failed: ") +
+                             dymu_last_error(ctx_));
+  node_state_.swap(closed);
+  band_cells_.clear();
+  for (const uint64_t k : order)
+    if (in_band[k]) band_cells_.push_back(k);  // the reference's band vector, in order
+  propagated_extra_.swap(order);
+  manual_list_ = true;
+  solved_ = false;
+  return band > 0;  // :399-407
 }
 
 // :443-468

@@ -52,6 +52,18 @@ __global__ void k_window_min(const double* T, int64_t ld, uint32_t i0, uint32_t 
   if (threadIdx.x == 0 && s_min != kInfBits) atomicMin(out, s_min);
 }
 
+// number of cells whose value is bitwise `value` (early-exit tie detection)
+__global__ void k_count_equal(const double* T, int64_t ld, uint32_t nx, uint32_t ny,
+                              unsigned long long vbits, unsigned long long* out) {
+  const uint64_t n = (uint64_t)nx * ny;
+  unsigned long long c = 0;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+       k += (uint64_t)gridDim.x * blockDim.x)
+    c += dbits(T[(int64_t)(k / nx) * ld + (int64_t)(k % nx)]) == vbits ? 1u : 0u;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
 // Reset every cell with old T >= theta (except the goal) and seed the tiles
 // holding a reset, finite-speed cell next to a kept finite cell.  A neighbour
 // read may race with its reset, but "old < theta" cells are never written, so
@@ -355,6 +367,16 @@ hipError_t launch_window_min(const double* T, int64_t ld, uint32_t i0, uint32_t 
   if (b > 1024) b = 1024;
   if (b == 0) b = 1;
   hipLaunchKernelGGL(k_window_min, dim3((unsigned)b), dim3(256), 0, st, T, ld, i0, j0, i1, j1, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_equal(const double* T, int64_t ld, uint32_t nx, uint32_t ny, double value,
+                              unsigned long long* out, hipStream_t st) {
+  uint64_t b = ((uint64_t)nx * ny + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b == 0) b = 1;
+  hipLaunchKernelGGL(k_count_equal, dim3((unsigned)b), dim3(256), 0, st, T, ld, nx, ny,
+                     (unsigned long long)__builtin_bit_cast(unsigned long long, value), out);
   return hipGetLastError();
 }
 

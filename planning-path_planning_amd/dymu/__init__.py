@@ -125,6 +125,8 @@ FIM_SYMBOLS = {
     "dymu_dom_round_supported": (_i32, [_vp, _u32]),
     "dymu_dom_round": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp]),
     "dymu_dom_round_peer": (_i32, [_vp, _u32, _vp, _vp]),
+    "dymu_count_equal": (_i32, [_vp, _vp, _u32, _u32, _u64, ctypes.c_double,
+                                ctypes.POINTER(_u64), _vp]),
     "dymu_dom_post_status": (_i32, [_vp, _vp, _vp, _u32]),
     "dymu_dom_post": (_i32, [_vp, _vp, ctypes.POINTER(_u32)]),
     "dymu_dom_wait_post": (_i32, [_vp, _u32, ctypes.c_double, ctypes.POINTER(ctypes.c_int32),

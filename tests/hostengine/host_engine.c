@@ -139,6 +139,16 @@ int dymu_early_exit_mask(dymu_ctx* c, const double* F, double* T, uint32_t nx, u
   *nb = n;
   return DYMU_OK;
 }
+int dymu_count_equal(dymu_ctx* c, const double* T, uint32_t nx, uint32_t ny, uint64_t ld,
+                     double v, uint64_t* count, void* s) {
+  (void)s;
+  if (!c || !count) return DYMU_ERR_ARG;
+  uint64_t n = 0;
+  for (uint32_t j = 0; j < ny; ++j)
+    for (uint32_t i = 0; i < nx; ++i) n += memcmp(&T[(uint64_t)j * ld + i], &v, sizeof v) == 0;
+  *count = n;
+  return DYMU_OK;
+}
 int dymu_scatter(dymu_ctx* c, double* T, uint32_t nx, uint64_t ld, const uint64_t* idx,
                  const double* v, uint64_t n, void* s) {
   (void)s;

@@ -255,6 +255,37 @@ def test_config1_exact_call(dymu, oracle, inputs):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N,g,s", [(160, (80, 80), (20, 140)), (512, (256, 256), (102, 128))])
+def test_early_exit_ties_exact(dymu, oracle, N, g, s):
+    """computeTotalCostMap on a constant-speed map, where every axis distance ties
+    with many others: which of the cells of exactly the exit value the reference
+    closed, and so which band cells it reached, depends on its insertion order.  The
+    planner detects the ties (dymu_count_equal, the band replay) and replays the
+    reference exactly on the host: the whole getTotalCostMatrix, every node state,
+    the band (in the reference's insertion order: its first node is the earliest
+    inserted) and the return value are the reference's (linear band, :551-568)."""
+    F = np.ones((N, N))
+    p = dymu.Planner()
+    try:
+        p.initGlobalLayer(1.0, 0.5, N, N)
+        p.setCostMap(F)
+        assert p.setGoal(g)
+        Tl, rc, closed = oracle.fmm(F, g, start=s, linear=True, want_closed=True)
+        assert p.computeTotalCostMap(s) == bool(rc)
+        M = p.getTotalCostMatrix()
+        want = np.where(np.isfinite(Tl), Tl, -1.0)
+        assert np.array_equal(M.view(np.uint64), want.view(np.uint64))
+        band = (closed == 0) & np.isfinite(Tl)
+        assert p.lastBandSize() == int(band.sum())
+        nb = p.globalNarrowband()
+        assert len(nb) == int(band.sum()) and all(band[j, i] for i, j in nb[:200])
+        for (i, j) in [s, g, (s[0] + 1, s[1]), tuple(nb[0]), tuple(nb[-1])]:
+            assert p.getGlobalNode(int(i), int(j))["state"] == int(closed[j, i])
+    finally:
+        p.close()
+
+
+@pytest.mark.gpu
 def test_early_exit_false_returns(dymu, oracle):
     """The reference returns false when the band is empty at exit (:399-403):
     a start enclosed by obstacles (unreachable), and a start whose neighbourhood
