@@ -68,6 +68,7 @@
 #include <vector>
 
 #include "fim_kernels.h"
+#include "peer_rule.hpp"
 
 namespace {
 
@@ -782,9 +783,7 @@ class PeerTransport final : public BoardTransport {
   int exchange(std::vector<Local>&, uint32_t, hipStream_t, std::string*) override { return DYMU_OK; }
   int reduce(int, hipStream_t, std::string*) override { return DYMU_OK; }
 
-  struct Status {
-    uint64_t P = 0, S[2] = {0, 0}, R[2] = {0, 0};
-  };
+  using Status = dymu_peer::Status;
   // the rounds; the domain is live on entry
   int run(Local& l, uint32_t nx, uint32_t ny, uint32_t K, hipStream_t st, std::string* err,
           uint64_t* rounds_out) {
@@ -848,17 +847,8 @@ class PeerTransport final : public BoardTransport {
           sq.R[side] = board[q].stat[k % 4][3 + side].load(std::memory_order_relaxed);
         }
       }
-      bool quiet = true, same = true;
-      for (int q = 0; q < world; ++q) {
-        quiet = quiet && cur[q].P == 0;
-        // link q -> q+1: q's pushes to rank+1 (side 1) against q+1's merges of rank-1 (side 0)
-        if (q + 1 < world) {
-          quiet = quiet && cur[q].S[1] == cur[q + 1].R[0] && cur[q + 1].S[0] == cur[q].R[1];
-        }
-        same = same && cur[q].S[0] == prev[q].S[0] && cur[q].S[1] == prev[q].S[1];
-      }
-      done = quiet && prev_quiet && same;
-      prev_quiet = quiet;
+      done = dymu_peer::done(prev, prev_quiet, cur);  // csrc/peer_rule.hpp
+      prev_quiet = dymu_peer::quiet(cur);
       prev.swap(cur);
     }
     *rounds_out = m;
