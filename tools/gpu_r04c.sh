@@ -10,3 +10,6 @@ DYMU_PRIO_TRACE=3000 timeout -k 10 300 python tools/maze_bench.py 4096 64 1 > $O
 python tools/trace_show.py $O/maze_trace.log
 DYMU_PRIO_TRACE=1000 timeout -k 10 300 python tools/maze_bench.py 4096 64 1 > $O/maze4096b.json 2> $O/maze_trace_b.log || { tail $O/maze_trace_b.log; exit 1; }
 python tools/trace_show.py $O/maze_trace_b.log
+# the exact-tie early exit and the equal-count kernel (new this round)
+timeout -k 10 300 python -u -m pytest tests/test_planner.py -k "early_exit" -x -v --timeout 120 --timeout-method thread > $O/early_exit_tests.txt 2>&1 || { tail -30 $O/early_exit_tests.txt; exit 1; }
+tail -5 $O/early_exit_tests.txt
