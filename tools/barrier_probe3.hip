@@ -11,6 +11,9 @@
 //   xcd0    W workgroups with block id % 8 == 0 (one XCD; the other blocks of the
 //           launch exit at once), plain stores, the barrier's own agent-scope
 //           atomics, then a vector-L1 invalidate (buffer_inv sc0) before the loads
+//   spread-L1  (control) W workgroups over the XCDs, plain stores, L1 invalidate only:
+//           a reader on another XCD keeps its own L2's stale line, so stale reads here
+//           and none under "xcd0 + L1 invalidate" show the W workgroups share one L2
 // Every round each workgroup writes a word with a PLAIN store and reads its
 // neighbour's with a PLAIN load after the barrier; a stale read sets a flag.
 // Every spin has a bailout (100 ms).
@@ -35,12 +38,13 @@ __global__ __launch_bounds__(1024) void k_empty(unsigned* out, unsigned p) {
 }
 
 // bar: [0] generation, [32] arrival counter, [64] error flags
-// MODE 0: spread + agent fences; 1: xcd0 + L1 invalidate; 2: xcd0, no invalidate
+// MODE 0: spread + agent fences; 1: xcd0 + L1 invalidate; 2: xcd0, no invalidate;
+// 3: spread + L1 invalidate (control)
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_bar(unsigned* out, unsigned* bar, int n, int W) {
   const unsigned b = blockIdx.x;
   unsigned me;
-  if (MODE == 0) {
+  if (MODE == 0 || MODE == 3) {
     if (b >= (unsigned)W) return;
     me = b;
   } else {
@@ -69,7 +73,7 @@ __global__ __launch_bounds__(1024) void k_bar(unsigned* out, unsigned* bar, int 
         }
       }
       if (MODE == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      if (MODE == 1) asm volatile("buffer_inv sc0" ::: "memory");
+      if (MODE == 1 || MODE == 3) asm volatile("buffer_inv sc0" ::: "memory");
       const unsigned v = out[((me + 1) % (unsigned)W) * 32];  // plain load
       if (v < (unsigned)p + 1) atomicOr(flag, 2u);
     }
@@ -99,15 +103,17 @@ int main(int argc, char** argv) {
     std::printf("launch of %3d empty 1024-thread workgroups: %.3f us each\n", W, 1000.0 * ms / n);
   }
   for (int rep = 0; rep < 2; ++rep)
-    for (int mode = 0; mode < 3; ++mode)
+    for (int mode = 0; mode < 4; ++mode)
       for (int W : {4, 8, 16, 32}) {
         CK(hipMemsetAsync(bar, 0, sizeof(unsigned) * 128, st));
         CK(hipMemsetAsync(out, 0, sizeof(unsigned) * 32 * 256, st));
         int nn = n, ww = W;
-        const int blocks = mode == 0 ? W : 8 * W;
+        const int blocks = (mode == 0 || mode == 3) ? W : 8 * W;
         void* args[] = {&out, &bar, &nn, &ww};
-        const void* fn = mode == 0 ? (const void*)k_bar<0>
-                         : mode == 1 ? (const void*)k_bar<1> : (const void*)k_bar<2>;
+        const void* fn = mode == 0   ? (const void*)k_bar<0>
+                         : mode == 1 ? (const void*)k_bar<1>
+                         : mode == 2 ? (const void*)k_bar<2>
+                                     : (const void*)k_bar<3>;
         CK(hipEventRecord(e0, st));
         CK(hipLaunchCooperativeKernel(fn, dim3(blocks), dim3(1024), args, 0, st));
         CK(hipEventRecord(e1, st));
@@ -116,8 +122,10 @@ int main(int argc, char** argv) {
         unsigned h = 0;
         CK(hipMemcpy(&h, bar + 64, sizeof h, hipMemcpyDeviceToHost));
         std::printf("%s W=%2d: %.3f us per barrier (flags %u)\n",
-                    mode == 0 ? "spread + agent fences  " : mode == 1 ? "xcd0 + L1 invalidate   "
-                                                                      : "xcd0, no invalidate    ",
+                    mode == 0   ? "spread + agent fences  "
+                    : mode == 1 ? "xcd0 + L1 invalidate   "
+                    : mode == 2 ? "xcd0, no invalidate    "
+                                : "spread + L1 inv (ctrl) ",
                     W, 1000.0 * ms / n, h);
         if (h & 1u) return 2;
       }
