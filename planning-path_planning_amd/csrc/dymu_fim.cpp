@@ -75,7 +75,9 @@ struct dymu_ctx {
   uint32_t sparse_max = 0;
   uint32_t sparse_passes = 16;
   uint32_t sparse_wg = 32;
-  uint32_t sparse_fence = 0;  // DYMU_SPARSE_FENCE=1: agent-scope fences at the barrier
+  uint32_t sparse_fence = 1;  // agent-scope fences at the barrier (DYMU_SPARSE_FENCE=0: off)
+  uint32_t sparse_xcc = 0;    // DYMU_SPARSE_XCC=1: workgroups chosen by their XCC_ID register
+  uint32_t sparse_seq = 0;    // sparse launches of this context
   unsigned* d_bar = nullptr;  // the sparse kernel's barrier words (zeroed once)
 
   // tile workspace
@@ -550,8 +552,8 @@ int dom_launch_sparse(dymu_ctx* c, uint64_t K, hipStream_t st, uint32_t report_b
     return DYMU_ERR_NOT_CONVERGED;
   }
   if (!c->d_bar) {
-    HIPC(c, hipMalloc(&c->d_bar, 512));
-    HIPC(c, hipMemset(c->d_bar, 0, 512));
+    HIPC(c, hipMalloc(&c->d_bar, 1024));
+    HIPC(c, hipMemset(c->d_bar, 0, 1024));
   }
   SparseArgs s{};
   s.a = D.a;
@@ -574,7 +576,12 @@ int dom_launch_sparse(dymu_ctx* c, uint64_t K, hipStream_t st, uint32_t report_b
   s.xcd_stride = 8;
   s.bar = c->d_bar;
   s.agent_fence = c->sparse_fence;
-  HIPC(c, launch_sparse(s, (int)(s.xcd_stride * c->sparse_wg), st));
+  s.xcc_select = c->sparse_xcc;
+  s.nblk = c->sparse_wg;
+  s.launch = c->sparse_seq++;
+  // XCC selection: 16x the workgroups, so XCC 0 sees at least sparse_wg of them
+  const int blocks = (int)(s.xcd_stride * c->sparse_wg) * (c->sparse_xcc ? 2 : 1);
+  HIPC(c, launch_sparse(s, blocks, st));
   D.p += K;
   ++D.launches;
   ++D.sparse_launches;
@@ -718,7 +725,7 @@ int dom_finish(dymu_ctx* c, hipStream_t st, dymu_stats* stats, double ms) {
     unsigned flag = 0;
     HIPC(c, hipMemcpy(&flag, c->d_bar + 64, sizeof flag, hipMemcpyDeviceToHost));
     if (flag) {
-      HIPC(c, hipMemset(c->d_bar, 0, 512));
+      HIPC(c, hipMemset(c->d_bar, 0, 1024));
       c->last_error = "sparse passes: a workgroup barrier timed out (results invalid)";
       return DYMU_ERR_HIP;
     }
@@ -1227,6 +1234,7 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
     if (const char* kv = std::getenv("DYMU_SPARSE_PASSES"))
       c->sparse_passes = (uint32_t)std::min(4096l, std::max(1l, std::atol(kv)));
     if (const char* kv = std::getenv("DYMU_SPARSE_FENCE")) c->sparse_fence = std::atoi(kv) != 0;
+    if (const char* kv = std::getenv("DYMU_SPARSE_XCC")) c->sparse_xcc = std::atoi(kv) != 0;
     if (const char* kv = std::getenv("DYMU_SPARSE_WG"))
       c->sparse_wg = (uint32_t)std::min(32l, std::max(1l, std::atol(kv)));
   }

@@ -148,8 +148,14 @@ struct SparseArgs {
   uint32_t eb;           // epoch of pass p = eb + p + 2
   uint32_t report_base;  // a.report set: pass p posts report_base + p (0 -> 1)
   uint32_t xcd_stride;   // workgroups with block id % xcd_stride == 0 run the passes
-  unsigned* bar;         // [0] generation, [32] arrivals, [64] error flag (zeroed once)
+  unsigned* bar;         // 256 words: [0] generation, [32] arrivals, [64] error flag,
+                         // [96] / [128] XCC tickets of even / odd launches (zeroed once)
   uint32_t agent_fence;  // 1: agent-scope fences at the pass barrier too
+  // 1: the first nblk workgroups that read XCC_ID 0 run the passes (xcd_stride unused);
+  // launch: this context's sparse-launch count (the ticket word alternates with it)
+  uint32_t xcc_select;
+  uint32_t nblk;
+  uint32_t launch;
 };
 // list entries: the tile index in the low kPackShift bits; bits above: 0 = no bin
 // (seeding kernels, merges), else the key bin + 1 the entry was first inserted with

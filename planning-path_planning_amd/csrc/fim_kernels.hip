@@ -1626,11 +1626,35 @@ __device__ __forceinline__ bool xcd_barrier(unsigned* bar, uint32_t nblk, bool a
 
 // 8-wave workgroups, one per CU: 256 VGPRs per wave (the pass loop's live state on top
 // of the pass body's 122 spills at 128)
+// the XCC (XCD) this wave runs on: hardware register XCC_ID (hwreg 20), bits [3:0]
+__device__ __forceinline__ uint32_t xcc_id() {
+  return (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;
+}
+
 template <int WPB, bool APPROX>
 __global__ __launch_bounds__(64 * WPB, 1) void k_fim_sparse(SparseArgs s) {
-  if (blockIdx.x % s.xcd_stride != 0u) return;
-  const uint32_t bid = blockIdx.x / s.xcd_stride;
-  const uint32_t nblk = gridDim.x / s.xcd_stride;
+  uint32_t bid, nblk;
+  if (s.xcc_select) {
+    // the first nblk workgroups that find themselves on XCC 0 run the passes; the
+    // ticket word alternates per launch, and ticket 0 clears the next launch's
+    __shared__ uint32_t s_ticket;
+    if (threadIdx.x == 0) {
+      uint32_t t = ~0u;
+      if (xcc_id() == 0u) t = atomicAdd(s.bar + 96 + (s.launch & 1u) * 32, 1u);
+      if (t == 0u)
+        __hip_atomic_store(s.bar + 96 + ((s.launch + 1u) & 1u) * 32, 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      s_ticket = t;
+    }
+    __syncthreads();
+    bid = s_ticket;
+    nblk = s.nblk;
+    if (bid >= nblk) return;
+  } else {
+    if (blockIdx.x % s.xcd_stride != 0u) return;
+    bid = blockIdx.x / s.xcd_stride;
+    nblk = gridDim.x / s.xcd_stride;
+  }
   for (uint32_t k = 0; k < s.npass; ++k) {
     const uint64_t p = s.p0 + k;
     const uint32_t n = pass_dyn<WPB, APPROX, false, true>(s.a, SparseRot{s, p, (uint32_t)(p % 3u)},

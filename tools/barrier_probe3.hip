@@ -14,6 +14,10 @@
 //   spread-L1  (control) W workgroups over the XCDs, plain stores, L1 invalidate only:
 //           a reader on another XCD keeps its own L2's stale line, so stale reads here
 //           and none under "xcd0 + L1 invalidate" show the W workgroups share one L2
+//   xcc0-reg  W workgroups that READ their XCC id (hardware register XCC_ID) as 0 and
+//           draw a ticket below W; plain stores, L1 invalidate (co-location by
+//           construction instead of by block-id arithmetic)
+// Also prints which XCC each block id of a 256-block launch ran on.
 // Every round each workgroup writes a word with a PLAIN store and reads its
 // neighbour's with a PLAIN load after the barrier; a stale read sets a flag.
 // Every spin has a bailout (100 ms).
@@ -37,14 +41,32 @@ __global__ __launch_bounds__(1024) void k_empty(unsigned* out, unsigned p) {
   if (threadIdx.x == 0) out[blockIdx.x] = p;
 }
 
-// bar: [0] generation, [32] arrival counter, [64] error flags
+// the XCC (XCD) this wave runs on: hardware register XCC_ID (id 20), bits [3:0]
+__device__ __forceinline__ unsigned xcc_id() {
+  return (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;
+}
+
+__global__ void k_xcc(unsigned* out) {
+  if (threadIdx.x == 0) out[blockIdx.x] = xcc_id();
+}
+
+// bar: [0] generation, [32] arrival counter, [64] error flags, [96] tickets (mode 4)
 // MODE 0: spread + agent fences; 1: xcd0 + L1 invalidate; 2: xcd0, no invalidate;
-// 3: spread + L1 invalidate (control)
+// 3: spread + L1 invalidate (control); 4: xcc0 by register + L1 invalidate
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_bar(unsigned* out, unsigned* bar, int n, int W) {
   const unsigned b = blockIdx.x;
   unsigned me;
-  if (MODE == 0 || MODE == 3) {
+  __shared__ unsigned s_me;
+  if (MODE == 4) {
+    if (threadIdx.x == 0) {
+      s_me = ~0u;
+      if (xcc_id() == 0u) s_me = atomicAdd(bar + 96, 1u);
+    }
+    __syncthreads();
+    me = s_me;
+    if (me >= (unsigned)W) return;
+  } else if (MODE == 0 || MODE == 3) {
     if (b >= (unsigned)W) return;
     me = b;
   } else {
@@ -73,7 +95,7 @@ __global__ __launch_bounds__(1024) void k_bar(unsigned* out, unsigned* bar, int 
         }
       }
       if (MODE == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      if (MODE == 1 || MODE == 3) asm volatile("buffer_inv sc0" ::: "memory");
+      if (MODE == 1 || MODE == 3 || MODE == 4) asm volatile("buffer_inv sc0" ::: "memory");
       const unsigned v = out[((me + 1) % (unsigned)W) * 32];  // plain load
       if (v < (unsigned)p + 1) atomicOr(flag, 2u);
     }
@@ -102,18 +124,35 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     std::printf("launch of %3d empty 1024-thread workgroups: %.3f us each\n", W, 1000.0 * ms / n);
   }
+  {
+    unsigned h[256];
+    hipLaunchKernelGGL(k_xcc, dim3(256), dim3(1024), 0, st, out);
+    CK(hipStreamSynchronize(st));
+    CK(hipMemcpy(h, out, sizeof h, hipMemcpyDeviceToHost));
+    std::printf("XCC of block ids 0..31:");
+    for (int b = 0; b < 32; ++b) std::printf(" %u", h[b]);
+    int per[16] = {0}, mod_ok = 0;
+    for (int b = 0; b < 256; ++b) {
+      ++per[h[b] & 15u];
+      mod_ok += h[b] == h[b % 8];
+    }
+    std::printf("\nblocks per XCC:");
+    for (int x = 0; x < 8; ++x) std::printf(" %d", per[x]);
+    std::printf("; blocks with the XCC of block id %% 8: %d / 256\n", mod_ok);
+  }
   for (int rep = 0; rep < 2; ++rep)
-    for (int mode = 0; mode < 4; ++mode)
+    for (int mode = 0; mode < 5; ++mode)
       for (int W : {4, 8, 16, 32}) {
         CK(hipMemsetAsync(bar, 0, sizeof(unsigned) * 128, st));
         CK(hipMemsetAsync(out, 0, sizeof(unsigned) * 32 * 256, st));
         int nn = n, ww = W;
-        const int blocks = (mode == 0 || mode == 3) ? W : 8 * W;
+        const int blocks = (mode == 0 || mode == 3) ? W : mode == 4 ? 256 : 8 * W;
         void* args[] = {&out, &bar, &nn, &ww};
         const void* fn = mode == 0   ? (const void*)k_bar<0>
                          : mode == 1 ? (const void*)k_bar<1>
                          : mode == 2 ? (const void*)k_bar<2>
-                                     : (const void*)k_bar<3>;
+                         : mode == 3 ? (const void*)k_bar<3>
+                                     : (const void*)k_bar<4>;
         CK(hipEventRecord(e0, st));
         CK(hipLaunchCooperativeKernel(fn, dim3(blocks), dim3(1024), args, 0, st));
         CK(hipEventRecord(e1, st));
@@ -125,7 +164,8 @@ int main(int argc, char** argv) {
                     mode == 0   ? "spread + agent fences  "
                     : mode == 1 ? "xcd0 + L1 invalidate   "
                     : mode == 2 ? "xcd0, no invalidate    "
-                                : "spread + L1 inv (ctrl) ",
+                    : mode == 3 ? "spread + L1 inv (ctrl) "
+                                : "xcc0-reg + L1 invalid. ",
                     W, 1000.0 * ms / n, h);
         if (h & 1u) return 2;
       }
