@@ -68,17 +68,6 @@ struct dymu_ctx {
   unsigned long long* arm_dst = nullptr;       // another post target (the peer status ring)
   const unsigned long long* arm_ext = nullptr;  // ... with these 4 status words
   int prio_debug = 0;        // v4: print the state after the first N passes (DYMU_PRIO_DEBUG)
-  // sparse passes (kernel 5, converge_stream): while the last posted list
-  // holds at most sparse_max tiles, the host queues launches of k_fim_sparse that run
-  // sparse_passes passes each on sparse_wg workgroups of one XCD.  sparse_max = 0: off.
-  // DYMU_SPARSE_MAX / DYMU_SPARSE_PASSES / DYMU_SPARSE_WG override.
-  uint32_t sparse_max = 0;
-  uint32_t sparse_passes = 16;
-  uint32_t sparse_wg = 32;
-  uint32_t sparse_fence = 1;  // agent-scope fences at the barrier (DYMU_SPARSE_FENCE=0: off)
-  uint32_t sparse_xcc = 0;    // DYMU_SPARSE_XCC=1: workgroups chosen by their XCC_ID register
-  uint32_t sparse_seq = 0;    // sparse launches of this context
-  unsigned* d_bar = nullptr;  // the sparse kernel's barrier words (zeroed once)
 
   // tile workspace
   uint32_t tiles_cap = 0;
@@ -124,8 +113,6 @@ struct dymu_ctx {
     uint32_t* lists[3] = {nullptr, nullptr, nullptr};
     uint32_t* counts[3] = {nullptr, nullptr, nullptr};
     size_t prof_used = 0;
-    uint64_t sparse_launches = 0;
-    uint32_t seed_listed = ~0u;  // tiles in list 0 if known (a cold solve: the goal's)
   } dom;
 
   // per-pass statistics (kernel 5; dymu_set_pass_stats): kPassStatCap records of
@@ -283,7 +270,6 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
     c->epoch_base = 0;
   }
   D.eb = c->epoch_base;
-  D.seed_listed = cold && gj >= 0 ? 1u : ~0u;
   c->epoch_base = D.eb + 4u;  // the seed's epoch stays used even if a step below fails
   const uint64_t lstride = (uint64_t)kShards * ntiles;
   for (int q = 0; q < 3; ++q) {
@@ -531,63 +517,6 @@ int dom_launch(dymu_ctx* c, uint64_t K, hipStream_t st, uint32_t report_seq = 0)
   return DYMU_OK;
 }
 
-// Sparse passes: K passes from D.p in one launch of k_fim_sparse (fim_kernels.hip) on
-// c->sparse_wg workgroups of one XCD -- the same passes dom_launch would queue (the
-// kernel derives the rotation, epoch and colour from the pass index); pass p posts
-// report_base + p when report_base != 0.  Not with per-pass profiling, statistics,
-// traces, deterministic mode or the in-pass merges of the sharded rounds.
-bool sparse_ok(const dymu_ctx* c) {
-  const auto& D = c->dom;
-  return c->sparse_max > 0 && D.live && D.variant == 5 && !D.rehist && !c->profiling &&
-         !c->pass_stats && c->prio_trace < 0 && c->prio_debug == 0 && !c->arm_seq &&
-         !D.a.merge_lo && !D.a.merge_hi && !D.a.peer && c->sparse_wg > 0;
-}
-
-int dom_launch_sparse(dymu_ctx* c, uint64_t K, hipStream_t st, uint32_t report_base) {
-  auto& D = c->dom;
-  if (!sparse_ok(c)) return DYMU_ERR_STATE;
-  if (D.p + K > D.max_passes + kPassSlack) {
-    c->last_error = "pass cap reached before convergence";
-    dom_retire(c);
-    return DYMU_ERR_NOT_CONVERGED;
-  }
-  if (!c->d_bar) {
-    HIPC(c, hipMalloc(&c->d_bar, 1024));
-    HIPC(c, hipMemset(c->d_bar, 0, 1024));
-  }
-  SparseArgs s{};
-  s.a = D.a;
-  s.a.report = report_base ? c->d_mail : nullptr;
-  s.a.report_src = nullptr;
-  s.a.report_ext = nullptr;
-  s.a.sweep_deadline = 0;  // a few visits per pass: no pass is ended by its slowest SIMDs
-  s.list0 = D.lists[0];
-  s.list_stride = (uint64_t)(D.lists[1] - D.lists[0]);
-  s.count0 = D.counts[0];
-  s.key0 = prio_keys(c, 0);
-  s.key_stride = D.ntiles;
-  s.hist0 = prio_hist(c, 0);
-  s.minkey0 = prio_minkey(c, 0);
-  s.base0 = prio_base(c, 0);
-  s.p0 = D.p;
-  s.npass = (uint32_t)K;
-  s.eb = D.eb;
-  s.report_base = report_base;
-  s.xcd_stride = 8;
-  s.bar = c->d_bar;
-  s.agent_fence = c->sparse_fence;
-  s.xcc_select = c->sparse_xcc;
-  s.nblk = c->sparse_wg;
-  s.launch = c->sparse_seq++;
-  // XCC selection: 16x the workgroups, so XCC 0 sees at least sparse_wg of them
-  const int blocks = (int)(s.xcd_stride * c->sparse_wg) * (c->sparse_xcc ? 2 : 1);
-  HIPC(c, launch_sparse(s, blocks, st));
-  D.p += K;
-  ++D.launches;
-  ++D.sparse_launches;
-  return DYMU_OK;
-}
-
 // tiles queued for the next pass (synchronises the stream)
 int dom_pending(dymu_ctx* c, hipStream_t st, uint64_t* out) {
   auto& D = c->dom;
@@ -721,15 +650,6 @@ int dom_finish(dymu_ctx* c, hipStream_t st, dymu_stats* stats, double ms) {
   if (!D.live) return DYMU_ERR_STATE;
   dom_retire(c);
   HIPC(c, hipStreamSynchronize(st));
-  if (D.sparse_launches) {  // a sparse launch whose barrier timed out left a flag
-    unsigned flag = 0;
-    HIPC(c, hipMemcpy(&flag, c->d_bar + 64, sizeof flag, hipMemcpyDeviceToHost));
-    if (flag) {
-      HIPC(c, hipMemset(c->d_bar, 0, 1024));
-      c->last_error = "sparse passes: a workgroup barrier timed out (results invalid)";
-      return DYMU_ERR_HIP;
-    }
-  }
   c->last_launches = D.launches;
   c->last_pass_ms = 0.0;
   c->last_timed = 0;
@@ -909,16 +829,8 @@ int converge_stream(dymu_ctx* c, hipStream_t st, dymu_stats* stats,
   const uint64_t ahead = c->max_batch;
   const uint32_t base = c->mail_seq + 1;  // pass p posts base + p
   auto post_seq = [&](uint64_t p) { uint32_t s = base + (uint32_t)p; return s ? s : 1u; };
-  // a list of at most sparse_max tiles (the last one posted): the next passes run as
-  // sparse launches (dom_launch_sparse), each posting every pass like single launches
-  const bool sparse = sparse_ok(c);
-  auto queue = [&](uint32_t listed) {
-    if (sparse && listed <= c->sparse_max) return dom_launch_sparse(c, c->sparse_passes, st, base);
-    return dom_launch(c, 1, st, post_seq(D.p));
-  };
   int rc = DYMU_OK;
-  const uint64_t p_start = D.p;
-  while (rc == DYMU_OK && D.p < p_start + ahead) rc = queue(D.seed_listed);
+  for (uint64_t k = 0; k < ahead && rc == DYMU_OK; ++k) rc = dom_launch(c, 1, st, post_seq(D.p));
   uint64_t running = 0;  // pass whose post the host waits for
   while (rc == DYMU_OK) {
     uint32_t pending = 0, seen = 0;
@@ -931,7 +843,7 @@ int converge_stream(dymu_ctx* c, hipStream_t st, dymu_stats* stats,
       rc = DYMU_ERR_NOT_CONVERGED;
       break;
     }
-    while (rc == DYMU_OK && D.p < running + 1 + ahead) rc = queue(pending & 0x7FFFFFFFu);
+    while (rc == DYMU_OK && D.p < running + 1 + ahead) rc = dom_launch(c, 1, st, post_seq(D.p));
     ++running;
   }
   c->mail_seq = base + (uint32_t)D.p + 1;
@@ -1230,13 +1142,6 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
     if (const char* kv = std::getenv("DYMU_PRUNE")) c->prune = std::atoi(kv);
     if (const char* kv = std::getenv("DYMU_PRIO_DEBUG")) c->prio_debug = std::atoi(kv);
     if (const char* kv = std::getenv("DYMU_RAISE")) c->raise = std::atoi(kv);
-    if (const char* kv = std::getenv("DYMU_SPARSE_MAX")) c->sparse_max = (uint32_t)std::atol(kv);
-    if (const char* kv = std::getenv("DYMU_SPARSE_PASSES"))
-      c->sparse_passes = (uint32_t)std::min(4096l, std::max(1l, std::atol(kv)));
-    if (const char* kv = std::getenv("DYMU_SPARSE_FENCE")) c->sparse_fence = std::atoi(kv) != 0;
-    if (const char* kv = std::getenv("DYMU_SPARSE_XCC")) c->sparse_xcc = std::atoi(kv) != 0;
-    if (const char* kv = std::getenv("DYMU_SPARSE_WG"))
-      c->sparse_wg = (uint32_t)std::min(32l, std::max(1l, std::atol(kv)));
   }
   if (e == hipSuccess) e = hipMalloc(&c->d_counts, sizeof(uint32_t) * 4 * kShards);
   if (e == hipSuccess) e = hipMalloc(&c->d_scratch, sizeof(unsigned long long) * 8);
@@ -1282,7 +1187,6 @@ int dymu_destroy(dymu_ctx* c) {
   if (c->d_ec) (void)hipFree(c->d_ec);
   if (c->d_lut) (void)hipFree(c->d_lut);
   if (c->d_scratch) (void)hipFree(c->d_scratch);
-  if (c->d_bar) (void)hipFree(c->d_bar);
   if (c->d_xchg) (void)hipFree(c->d_xchg);
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->d_F) (void)hipFree(c->d_F);

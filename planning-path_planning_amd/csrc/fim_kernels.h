@@ -128,35 +128,6 @@ struct PassArgs {
   // is never above the first-insertion one, so the decision is the key gate's)
   int pack_bins;
 };
-// sparse passes (kernel 5, fim_kernels.hip k_fim_sparse): npass passes from p0 in one
-// launch, with the 3-buffer rotation of dom_launch computed on the device
-constexpr int kSparseWaves = 8;  // waves per workgroup of the sparse kernel
-struct SparseArgs {
-  PassArgs a;  // everything but the rotated buffers, epoch, parity and report_seq
-  // buffer q of the rotation (dom_begin's layout; strides, not arrays: an array
-  // indexed by p % 3 would put the whole argument block in scratch)
-  uint32_t* list0;             // list q = list0 + q * list_stride
-  uint64_t list_stride;
-  uint32_t* count0;            // counts q = count0 + q * kShards
-  unsigned long long* key0;    // keys q = key0 + q * key_stride
-  uint64_t key_stride;
-  uint32_t* hist0;             // histogram q = hist0 + q * kShards * kBins
-  unsigned long long* minkey0; // min key q = minkey0 + q
-  double* base0;               // origin q = base0 + q
-  uint64_t p0;
-  uint32_t npass;
-  uint32_t eb;           // epoch of pass p = eb + p + 2
-  uint32_t report_base;  // a.report set: pass p posts report_base + p (0 -> 1)
-  uint32_t xcd_stride;   // workgroups with block id % xcd_stride == 0 run the passes
-  unsigned* bar;         // 256 words: [0] generation, [32] arrivals, [64] error flag,
-                         // [96] / [128] XCC tickets of even / odd launches (zeroed once)
-  uint32_t agent_fence;  // 1: agent-scope fences at the pass barrier too
-  // 1: the first nblk workgroups that read XCC_ID 0 run the passes (xcd_stride unused);
-  // launch: this context's sparse-launch count (the ticket word alternates with it)
-  uint32_t xcc_select;
-  uint32_t nblk;
-  uint32_t launch;
-};
 // list entries: the tile index in the low kPackShift bits; bits above: 0 = no bin
 // (seeding kernels, merges), else the key bin + 1 the entry was first inserted with
 constexpr int kPackShift = 25;
@@ -193,8 +164,6 @@ hipError_t launch_pass_prio(const PassArgs& a, int blocks, hipStream_t st,
                            hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_pass_prio16(const PassArgs& a, int blocks, hipStream_t st,
                              hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);  // kernel 5
-// blocks = xcd_stride x the workgroups that run the passes
-hipError_t launch_sparse(const SparseArgs& s, int blocks, hipStream_t st);
 hipError_t launch_pass_rb(const PassArgs& a, int blocks, hipStream_t st,
                       hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);     // v3: 2 x 8x8 tiles / wave, red-black
 hipError_t launch_merge_ghosts(double* T, int64_t ld, int64_t nx, int64_t nrows,

@@ -336,47 +336,32 @@ __device__ __forceinline__ int rb_sweeps(double* img, int sr, int sb, double fr,
   return sweeps;
 }
 
-// A word that other workgroups of the SAME launch write (the sparse kernel's passes):
-// an atomic load, which is never served from the scalar cache, and after the pass
-// barrier's vector-L1 invalidate reads the XCD's L2.  LIVE = false: a plain load.
-template <bool LIVE, class W>
-__device__ __forceinline__ W ld_live(const W* p) {
-  if constexpr (LIVE) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else return *p;
-}
-
 // the convergence mailbox (PassArgs::report): a system-scope vector store into
 // host-coherent memory, visible to a polling host thread while the stream runs
-template <bool LIVE>
-__device__ __forceinline__ void report_pending(const PassArgs& a, uint32_t n_active,
-                                               uint32_t report_seq,
-                                               const unsigned long long* minkey_in) {
+__device__ __forceinline__ void report_pending(const PassArgs& a, uint32_t n_active) {
   if (a.report) {
     uint32_t v = a.report_src ? (uint32_t)*a.report_src : n_active;
     if (a.probe.n > 0 && a.minkey_in) {  // T, keys >= 0: bit order = value order
       unsigned long long tmax = 0;
       for (int k = 0; k < a.probe.n; ++k) {
         const unsigned long long b =
-            __double_as_longlong(ld_live<LIVE>(a.T + a.probe.ij[k][1] * a.ld + a.probe.ij[k][0]));
+            __double_as_longlong(a.T[a.probe.ij[k][1] * a.ld + a.probe.ij[k][0]]);
         tmax = b > tmax ? b : tmax;
       }
-      if (ld_live<LIVE>(minkey_in) > tmax) v |= 0x80000000u;
+      if (*a.minkey_in > tmax) v |= 0x80000000u;
     }
     if (a.report_ext) {  // the status words first, then the word the host polls
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         __hip_atomic_store(a.report + 1 + k, a.report_ext[k], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(a.report, ((unsigned long long)report_seq << 32) | v, __ATOMIC_RELEASE,
+      __hip_atomic_store(a.report, ((unsigned long long)a.report_seq << 32) | v, __ATOMIC_RELEASE,
                          __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
-    __hip_atomic_store(a.report, ((unsigned long long)report_seq << 32) | v, __ATOMIC_RELAXED,
+    __hip_atomic_store(a.report, ((unsigned long long)a.report_seq << 32) | v, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
-}
-__device__ __forceinline__ void report_pending(const PassArgs& a, uint32_t n_active) {
-  report_pending<false>(a, n_active, a.report_seq, a.minkey_in);
 }
 
 // ---- peer rounds (dymu_dom_round_peer; DESIGN.md s5 "Peer transport") ----
@@ -1206,72 +1191,8 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_prio(PassArgs a) {
 // STATS: the per-pass statistics (a.pstat) are counted -- a separate instantiation,
 // so the default kernel carries none of it (it cost 2% per solve inline: SGPR
 // spills 31 -> 41, profiles/r03/knobs1)
-// The buffers and scalars that rotate from pass to pass (dom_launch's 3-buffer
-// rotation, epoch, colour, mailbox sequence): read through these so the dense kernel
-// takes them from its arguments and the sparse kernel derives them from the pass
-// index without keeping a mutable copy of PassArgs live (registers: the copy spilled).
-struct DenseRot {
-  const PassArgs& a;
-  __device__ const uint32_t* list_in() const { return a.list_in; }
-  __device__ const uint32_t* count_in() const { return a.count_in; }
-  __device__ uint32_t* list_out() const { return a.list_out; }
-  __device__ uint32_t* count_out() const { return a.count_out; }
-  __device__ uint32_t* count_clear() const { return a.count_clear; }
-  __device__ unsigned long long* key_in() const { return a.key_in; }
-  __device__ unsigned long long* key_out() const { return a.key_out; }
-  __device__ const uint32_t* hist_in() const { return a.hist_in; }
-  __device__ uint32_t* hist_out() const { return a.hist_out; }
-  __device__ uint32_t* hist_clear() const { return a.hist_clear; }
-  __device__ const unsigned long long* minkey_in() const { return a.minkey_in; }
-  __device__ unsigned long long* minkey_out() const { return a.minkey_out; }
-  __device__ unsigned long long* minkey_clear() const { return a.minkey_clear; }
-  __device__ const double* base_in() const { return a.base_in; }
-  __device__ double* base_out() const { return a.base_out; }
-  __device__ uint32_t epoch() const { return a.epoch; }
-  __device__ uint32_t checker_parity() const { return a.checker_parity; }
-  __device__ uint32_t report_seq() const { return a.report_seq; }
-};
-
-struct SparseRot {
-  const SparseArgs& s;
-  uint64_t p;
-  uint32_t r;  // p % 3
-  __device__ uint32_t r1() const { return r == 2u ? 0u : r + 1u; }
-  __device__ uint32_t r2() const { return r == 0u ? 2u : r - 1u; }
-  __device__ uint32_t* list(uint32_t q) const { return s.list0 + q * s.list_stride; }
-  __device__ uint32_t* count(uint32_t q) const { return s.count0 + q * kShards; }
-  __device__ unsigned long long* key(uint32_t q) const { return s.key0 + q * s.key_stride; }
-  __device__ uint32_t* hist(uint32_t q) const { return s.hist0 + q * (kShards * kBins); }
-  __device__ const uint32_t* list_in() const { return list(r); }
-  __device__ const uint32_t* count_in() const { return count(r); }
-  __device__ uint32_t* list_out() const { return list(r1()); }
-  __device__ uint32_t* count_out() const { return count(r1()); }
-  __device__ uint32_t* count_clear() const { return count(r2()); }
-  __device__ unsigned long long* key_in() const { return key(r); }
-  __device__ unsigned long long* key_out() const { return key(r1()); }
-  __device__ const uint32_t* hist_in() const { return hist(r); }
-  __device__ uint32_t* hist_out() const { return hist(r1()); }
-  __device__ uint32_t* hist_clear() const { return hist(r2()); }
-  __device__ const unsigned long long* minkey_in() const { return s.minkey0 + r; }
-  __device__ unsigned long long* minkey_out() const { return s.minkey0 + r1(); }
-  __device__ unsigned long long* minkey_clear() const { return s.minkey0 + r2(); }
-  __device__ const double* base_in() const { return s.base0 + r; }
-  __device__ double* base_out() const { return s.base0 + r1(); }
-  __device__ uint32_t epoch() const { return s.eb + (uint32_t)p + 2u; }
-  __device__ uint32_t checker_parity() const { return (uint32_t)(p & 1u); }
-  __device__ uint32_t report_seq() const {
-    const uint32_t q = s.report_base + (uint32_t)p;
-    return q ? q : 1u;
-  }
-};
-
-template <int WPB, bool APPROX, bool STATS, bool SPARSE, class Rot>
-__device__ __forceinline__ uint32_t pass_dyn(const PassArgs& a, const Rot& R, const uint32_t bid,
-                                             const uint32_t nblk) {
-  // the dense kernel reads the launch's own ids where it uses them (as before the body
-  // became a function: hoisting them costs SGPRs); the sparse kernel passes its own
-  const auto wg_id = [&]() -> uint32_t { return SPARSE ? bid : blockIdx.x; };
-  const auto wg_count = [&]() -> uint32_t { return SPARSE ? nblk : gridDim.x; };
+template <int WPB, bool APPROX, bool STATS = false>
+__global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   constexpr int IMG = IMG16;
   __shared__ uint32_t s_q[QCAP];
   __shared__ uint32_t s_pref[kShards + 1];
@@ -1287,21 +1208,21 @@ __device__ __forceinline__ uint32_t pass_dyn(const PassArgs& a, const Rot& R, co
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
-  const uint32_t shard = wg_id() % kShards;
-  unsigned long long* trace = a.trace ? a.trace + (uint64_t)wg_id() * kTracePts : nullptr;
+  const uint32_t shard = blockIdx.x % kShards;
+  unsigned long long* trace = a.trace ? a.trace + (uint64_t)blockIdx.x * kTracePts : nullptr;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   const unsigned long long stop_at = a.sweep_deadline ? t_start + a.sweep_deadline : ~0ull;
   if (trace && tid == 0) trace[0] = t_start;
 
   const double delta = *a.delta;
-  const double origin_in = ld_live<SPARSE>(R.base_in());
-  const double origin_out = bitsd(ld_live<SPARSE>(R.minkey_in()));
+  const double origin_in = *a.base_in;
+  const double origin_out = bitsd(*a.minkey_in);
   const double inv_delta = 1.0 / delta;
   if (wv == 0) {  // shard prefix counts and the threshold bin (as k_fim_pass_prio)
-    uint32_t c = lane < kShards ? R.count_in()[lane] : 0u;
+    uint32_t c = lane < kShards ? a.count_in[lane] : 0u;
     uint32_t h = 0;
 #pragma unroll
-    for (int k = 0; k < kShards; ++k) h += R.hist_in()[k * kBins + lane];
+    for (int k = 0; k < kShards; ++k) h += a.hist_in[k * kBins + lane];
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t yc = __shfl_up(c, o), yh = __shfl_up(h, o);
@@ -1339,12 +1260,12 @@ __device__ __forceinline__ uint32_t pass_dyn(const PassArgs& a, const Rot& R, co
   const uint32_t n_active = s_pref[kShards];
   const int bstar = s_bstar;
   if (trace && tid == 0) trace[1] = __builtin_amdgcn_s_memrealtime();
-  if (wg_id() == 0) {
-    if (tid < kShards) R.count_clear()[tid] = 0u;
-    for (int k = tid; k < kShards * kBins; k += blockDim.x) R.hist_clear()[k] = 0u;
+  if (blockIdx.x == 0) {
+    if (tid < kShards) a.count_clear[tid] = 0u;
+    for (int k = tid; k < kShards * kBins; k += blockDim.x) a.hist_clear[k] = 0u;
     if (tid == 0) {
-      *R.minkey_clear() = kInfBits;
-      *R.base_out() = origin_out;
+      *a.minkey_clear = kInfBits;
+      *a.base_out = origin_out;
       if (n_active > 0) {
         atomicAdd(&a.stats[kStatPasses], 1ull);
         atomicMax(&a.stats[kStatMaxActive], (unsigned long long)n_active);
@@ -1353,7 +1274,7 @@ __device__ __forceinline__ uint32_t pass_dyn(const PassArgs& a, const Rot& R, co
         a.pstat[kPsActive] = n_active;
         a.pstat[kPsBstar] = (uint32_t)bstar;
       }
-      report_pending<SPARSE>(a, n_active, R.report_seq(), R.minkey_in());
+      report_pending(a, n_active);
       if (a.tot_save) *a.tot_save = n_active;
       if (a.tot_out) *a.tot_out = (int32_t)(*a.tot_prev + n_active);
       if (a.peer && a.tot_out) peer_status(a.peer);
@@ -1361,9 +1282,9 @@ __device__ __forceinline__ uint32_t pass_dyn(const PassArgs& a, const Rot& R, co
   }
 
   auto enqueue = [&](uint32_t t, unsigned long long kb) {
-    atomicMin(&R.key_out()[t], kb);
+    atomicMin(&a.key_out[t], kb);
     atomicMin(&s_minout, kb);
-    if (atomicMax(&a.tile_epoch[t], R.epoch()) < R.epoch()) {
+    if (atomicMax(&a.tile_epoch[t], a.epoch) < a.epoch) {
       const int bin = key_bin(bitsd(kb), origin_out, inv_delta);
       atomicAdd(&s_hout[bin], 1u);
       const uint32_t ent = a.pack_bins ? (t | ((uint32_t)(bin + 1) << kPackShift)) : t;
@@ -1371,8 +1292,8 @@ __device__ __forceinline__ uint32_t pass_dyn(const PassArgs& a, const Rot& R, co
       if (pos < QCAP) {
         s_q[pos] = ent;
       } else {
-        const uint32_t gp = atomicAdd(&R.count_out()[shard], 1u);
-        R.list_out()[(uint64_t)shard * a.shard_cap + gp] = ent;
+        const uint32_t gp = atomicAdd(&a.count_out[shard], 1u);
+        a.list_out[(uint64_t)shard * a.shard_cap + gp] = ent;
       }
     }
   };
@@ -1381,8 +1302,8 @@ __device__ __forceinline__ uint32_t pass_dyn(const PassArgs& a, const Rot& R, co
   uint32_t my_cd = 0, my_cap = 0, my_dl = 0, my_rmax = 0, my_rmin = ~0u;  // a.pstat only
   double* img = s_img[wv];
   unsigned long long* ek = s_ek[wv];
-  const uint32_t chunk = (n_active + wg_count() - 1) / wg_count();
-  const uint32_t c0 = wg_id() * chunk;
+  const uint32_t chunk = (n_active + gridDim.x - 1) / gridDim.x;
+  const uint32_t c0 = blockIdx.x * chunk;
   const uint32_t c1 = min(n_active, c0 + chunk);
   bool first = true;
   if (trace && tid == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
@@ -1392,28 +1313,28 @@ __device__ __forceinline__ uint32_t pass_dyn(const PassArgs& a, const Rot& R, co
     e = __builtin_amdgcn_readfirstlane(e);
     if (e >= c1) break;
     const uint32_t ent =
-        __builtin_amdgcn_readfirstlane(list_at_wave(R.list_in(), a.shard_cap, s_pref, e, lane));
+        __builtin_amdgcn_readfirstlane(list_at_wave(a.list_in, a.shard_cap, s_pref, e, lane));
     const uint32_t tile = ent & kTileMask;
     const int pbin = (int)(ent >> kPackShift) - 1;  // first-insertion bin, -1: none
     const int tx = (int)(tile % (uint32_t)a.ntx);
     const int ty = (int)(tile / (uint32_t)a.ntx);
-    if (a.checker && ((uint32_t)(tx + ty) + R.checker_parity()) % 2u != 0u) {
+    if (a.checker && ((uint32_t)(tx + ty) + a.checker_parity) % 2u != 0u) {
       // the other colour of the checkerboard: deferred with its key, tile not loaded
       if (lane == 0) {
-        const unsigned long long k0 = ld_live<SPARSE>(R.key_in() + tile);
-        R.key_in()[tile] = kInfBits;
+        const unsigned long long k0 = a.key_in[tile];
+        a.key_in[tile] = kInfBits;
         enqueue(tile, k0);
       }
       ++my_defer;
       if (STATS && a.pstat) ++my_cd;
       continue;
     }
-    const unsigned long long kb = ld_live<SPARSE>(R.key_in() + tile);
+    const unsigned long long kb = a.key_in[tile];
     // a packed bin at or below b*: admitted (the current key is no higher); above: the
     // current key decides now, before the tile loads a deferral would waste
     if (pbin > bstar && key_bin(bitsd(kb), origin_in, inv_delta) > bstar) {
       if (lane == 0) {
-        R.key_in()[tile] = kInfBits;
+        a.key_in[tile] = kInfBits;
         enqueue(tile, kb);
       }
       ++my_defer;
@@ -1426,7 +1347,7 @@ __device__ __forceinline__ uint32_t pass_dyn(const PassArgs& a, const Rot& R, co
     const int sweeps = visit16<APPROX>(
         a, img, ek, true, tx, ty, lane, capped,
         [&] { return decided || key_bin(bitsd(kb), origin_in, inv_delta) <= bstar; }, stop_at);
-    if (lane == 0) R.key_in()[tile] = kInfBits;
+    if (lane == 0) a.key_in[tile] = kInfBits;
     if (sweeps < 0) {  // deferred to the next pass with its key
       if (lane == 0) enqueue(tile, kb);
       ++my_defer;
@@ -1480,8 +1401,8 @@ __device__ __forceinline__ uint32_t pass_dyn(const PassArgs& a, const Rot& R, co
       // this workgroup's share of the columns (a whole number of 16-wide tiles): min-merge
       // the received rows into the ghost rows, queue the tile under each improved column
       // group with the smallest improved value as its key (as k_merge_ghosts)
-      const int64_t cw = (((int64_t)a.nx + wg_count() - 1) / wg_count() + 15) & ~(int64_t)15;
-      const int64_t m0 = (int64_t)wg_id() * cw;
+      const int64_t cw = (((int64_t)a.nx + gridDim.x - 1) / gridDim.x + 15) & ~(int64_t)15;
+      const int64_t m0 = (int64_t)blockIdx.x * cw;
       const int64_t m1 = min((int64_t)a.nx, m0 + cw);
       for (int side = 0; side < 2; ++side) {
         const double* src = side == 0 ? a.merge_lo : a.merge_hi;
@@ -1536,8 +1457,8 @@ __device__ __forceinline__ uint32_t pass_dyn(const PassArgs& a, const Rot& R, co
   __syncthreads();
   const uint32_t nq = s_nq < QCAP ? s_nq : QCAP;
   if (tid == 0) {
-    if (nq) s_base = atomicAdd(&R.count_out()[shard], nq);
-    if (s_minout != kInfBits) atomicMin(R.minkey_out(), s_minout);
+    if (nq) s_base = atomicAdd(&a.count_out[shard], nq);
+    if (s_minout != kInfBits) atomicMin(a.minkey_out, s_minout);
     if (s_visits || s_defer) {
       unsigned long long* st = a.stats + (uint64_t)shard * kStatSlots;
       atomicAdd(&st[kStatVisits], s_visits);
@@ -1557,109 +1478,13 @@ __device__ __forceinline__ uint32_t pass_dyn(const PassArgs& a, const Rot& R, co
       atomicAdd(&ps[kPsEnqueued], s_nq);
     }
   }
-  if (tid < kBins && s_hout[tid]) atomicAdd(&R.hist_out()[shard * kBins + tid], s_hout[tid]);
+  if (tid < kBins && s_hout[tid]) atomicAdd(&a.hist_out[shard * kBins + tid], s_hout[tid]);
   __syncthreads();
   for (uint32_t k = tid; k < nq; k += blockDim.x)
-    R.list_out()[(uint64_t)shard * a.shard_cap + s_base + k] = s_q[k];
+    a.list_out[(uint64_t)shard * a.shard_cap + s_base + k] = s_q[k];
   if (trace && tid == 0) {
     trace[4] = __builtin_amdgcn_s_memrealtime();
     trace[5] = ((unsigned long long)(c1 > c0 ? c1 - c0 : 0) << 32) | (unsigned long long)s_visits;
-  }
-  return n_active;
-}
-
-template <int WPB, bool APPROX, bool STATS = false>
-__global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
-  (void)pass_dyn<WPB, APPROX, STATS, false>(a, DenseRot{a}, blockIdx.x, gridDim.x);
-}
-
-// ---- sparse passes: many kernel-5 passes in ONE launch on one XCD ----
-// Hop-bound phases (short lists: the serpentine maze, windowed updates, early exits)
-// pay a launch per pass however little the pass holds.  Here the workgroups whose block
-// id is a multiple of xcd_stride (8: round-robin dispatch puts them all on XCD 0; the
-// others exit at once) run s.npass passes, the same passes the dense kernel would run
-// (pass_dyn, the 3-buffer rotation of dom_launch), separated by a barrier among them.
-// They share one L2, so a pass boundary needs no L2 write-back or invalidate: each wave
-// waits for its own stores, the barrier's atomics order the workgroups, and the
-// vector L1 is invalidated before the next pass reads.  Words the passes read with
-// uniform addresses are atomic loads (ld_live), never scalar-cache loads.
-// Every spin has a bound; a barrier that times out sets bar[64] and ends the launch
-// (the host fails the solve: dom_finish).
-
-// one barrier among nblk workgroups (thread 0 of each): bar[0] generation, bar[32]
-// arrivals, bar[64] error flag; false after a timeout
-// agent: release / acquire at agent scope as well (L2 write-back and invalidate: correct
-// wherever the workgroups run; DYMU_SPARSE_FENCE=1, A/B and fallback)
-__device__ __forceinline__ bool xcd_barrier(unsigned* bar, uint32_t nblk, bool agent) {
-  __builtin_amdgcn_s_waitcnt(0);  // this wave's stores have reached the L2
-  if (agent) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  __shared__ uint32_t s_ok;
-  if (threadIdx.x == 0) {
-    unsigned* gen = bar;
-    unsigned* cnt = bar + 32;
-    const unsigned g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_s_waitcnt(0);  // the generation is read before this arrival counts
-    if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1u) {
-      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_waitcnt(0);  // the reset before the release of the others
-      __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    uint32_t ok = 1u;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0) {
-      if (__hip_atomic_load(bar + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
-          __builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 200 ms
-        __hip_atomic_fetch_or(bar + 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0u;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (agent) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("buffer_inv sc0" ::: "memory");  // this CU's vector L1
-    s_ok = ok;
-  }
-  __syncthreads();
-  return s_ok != 0u;
-}
-
-// 8-wave workgroups, one per CU: 256 VGPRs per wave (the pass loop's live state on top
-// of the pass body's 122 spills at 128)
-// the XCC (XCD) this wave runs on: hardware register XCC_ID (hwreg 20), bits [3:0]
-__device__ __forceinline__ uint32_t xcc_id() {
-  return (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;
-}
-
-template <int WPB, bool APPROX>
-__global__ __launch_bounds__(64 * WPB, 1) void k_fim_sparse(SparseArgs s) {
-  uint32_t bid, nblk;
-  if (s.xcc_select) {
-    // the first nblk workgroups that find themselves on XCC 0 run the passes; the
-    // ticket word alternates per launch, and ticket 0 clears the next launch's
-    __shared__ uint32_t s_ticket;
-    if (threadIdx.x == 0) {
-      uint32_t t = ~0u;
-      if (xcc_id() == 0u) t = atomicAdd(s.bar + 96 + (s.launch & 1u) * 32, 1u);
-      if (t == 0u)
-        __hip_atomic_store(s.bar + 96 + ((s.launch + 1u) & 1u) * 32, 0u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      s_ticket = t;
-    }
-    __syncthreads();
-    bid = s_ticket;
-    nblk = s.nblk;
-    if (bid >= nblk) return;
-  } else {
-    if (blockIdx.x % s.xcd_stride != 0u) return;
-    bid = blockIdx.x / s.xcd_stride;
-    nblk = gridDim.x / s.xcd_stride;
-  }
-  for (uint32_t k = 0; k < s.npass; ++k) {
-    const uint64_t p = s.p0 + k;
-    const uint32_t n = pass_dyn<WPB, APPROX, false, true>(s.a, SparseRot{s, p, (uint32_t)(p % 3u)},
-                                                        bid, nblk);
-    if (!xcd_barrier(s.bar, nblk, s.agent_fence != 0u) || n == 0u) break;  // uniform: every workgroup read n
   }
 }
 
@@ -1932,20 +1757,6 @@ hipError_t launch_pass_prio16(const PassArgs& a, int blocks, hipStream_t st, hip
                         : launch_dyn_k<16, true, true>(a, blocks, st, e0, e1);
   return a.exact_sqrt ? launch_dyn_k<16, false>(a, blocks, st, e0, e1)
                       : launch_dyn_k<16, true>(a, blocks, st, e0, e1);
-}
-
-hipError_t launch_sparse(const SparseArgs& s, int blocks, hipStream_t st) {
-  if (s.a.pstat || s.a.trace || s.a.merge_lo || s.a.merge_hi || s.a.push_dst[0] || s.a.push_dst[1] ||
-      s.a.tot_out || s.a.tot_save || s.a.report_src || s.xcd_stride == 0u ||
-      blocks % (int)s.xcd_stride != 0)
-    return hipErrorInvalidValue;
-  // dynamic LDS the kernel does not use: with its static 45 KB, one workgroup per CU
-  constexpr size_t kPad = 48 * 1024;
-  if (s.a.exact_sqrt)
-    hipLaunchKernelGGL((k_fim_sparse<kSparseWaves, false>), dim3(blocks), dim3(64 * kSparseWaves), kPad, st, s);
-  else
-    hipLaunchKernelGGL((k_fim_sparse<kSparseWaves, true>), dim3(blocks), dim3(64 * kSparseWaves), kPad, st, s);
-  return hipGetLastError();
 }
 
 int pass_blocks_per_cu(int variant) {
