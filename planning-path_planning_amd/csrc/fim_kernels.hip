@@ -146,6 +146,13 @@ __device__ __forceinline__ double vmin64(double a, double b) {
   return r;
 }
 
+// min(|a|, b) in one v_min_f64 (abs source modifier); a NaN operand yields the other
+__device__ __forceinline__ double vmin64_abs(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, |%1|, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // Correctly rounded sqrt for x in [2^-767, 2^1023]: LLVM's f64 sqrt expansion
 // (rsq + Goldschmidt/Newton refinement) minus its range scaling and special-
 // value selects, which are identities on that range.  Bit-identical to sqrt()
@@ -222,33 +229,40 @@ __device__ __forceinline__ double two_sided_approx(double ty, double d, double c
 // up to those C-scale errors: the min over history is then the last
 // evaluation's value, and the map is the fixed point of the update rather
 // than its luckiest rounding (tools/mono_sim.c: the bias no longer grows with
-// the path length).  The one-sided value m + C is the reference's, bit for bit.
-// h of the approximate sweep sqrt: y0 = rsq(r), s = r*y0,
-// sqrt(r)/2 ~ s*(0.75 - (y0/4)*s), so h = fma(s, t, |d|/2)
-__device__ __forceinline__ double half_two_sided_approx(double d, double c2x2) {
-  const double r = __builtin_fma(-d, d, c2x2);
+// the path length).
+// The default sweep candidate (v33) also folds the branch into h's argument:
+// e = min(|Tx - Ty|, C), T' = m + h(e) -- the two-sided h below C, h(C) = (C +
+// sqrt(C^2)) / 2 ~ C at and above it (the one-sided value within the sweep sqrt's
+// 36 ulp of C instead of bit for bit; continuous and monotone across |d| = C) -- one
+// v_min_f64 instead of a compare and two selects.  The approximate sqrt: y0 =
+// rsq(r), s = r*y0, sqrt(r) ~ s*(1.5 - (y0/2)*s) (one Goldschmidt step); at twice
+// the scale, t2 = 1.5 - (y0/2) s, h2 = e + s t2 = 2h, T' = fma(h2, 0.5, m) = RN(m + h)
+// (scalings by 2 are exact) -- no e/2 multiply.  12 VALU per cell after the
+// neighbours' minima, 14 with them (v32: 16.5).  e >= 0.
+__device__ __forceinline__ double cand_approx(double e, double c2x2, double m) {
+  const double r = __builtin_fma(-e, e, c2x2);
   const double y0 = __builtin_amdgcn_rsq(r);
   const double s = r * y0;
-  const double t = __builtin_fma(-(y0 * 0.25), s, 0.75);
-  return __builtin_fma(s, t, fabs(d) * 0.5);
+  const double t2 = __builtin_fma(-(y0 * 0.5), s, 1.5);
+  return __builtin_fma(__builtin_fma(s, t2, e), 0.5, m);
 }
 
-// half_two_sided_approx on two independent cells, statement by statement
-// interleaved (same operations, bit-identical)
-__device__ __forceinline__ void half_two_sided_approx2(double d0, double c0, double d1, double c1,
-                                                       double& h0, double& h1) {
-  const double r0 = __builtin_fma(-d0, d0, c0);
-  const double r1 = __builtin_fma(-d1, d1, c1);
+// cand_approx on two independent cells, statement by statement interleaved (same
+// operations, bit-identical)
+__device__ __forceinline__ void cand_approx2(double e0, double c0, double m0, double e1, double c1,
+                                             double m1, double& u0, double& u1) {
+  const double r0 = __builtin_fma(-e0, e0, c0);
+  const double r1 = __builtin_fma(-e1, e1, c1);
   const double y0 = __builtin_amdgcn_rsq(r0);
   const double y1 = __builtin_amdgcn_rsq(r1);
-  const double a0 = fabs(d0) * 0.5;
-  const double a1 = fabs(d1) * 0.5;
   const double s0 = r0 * y0;
   const double s1 = r1 * y1;
-  const double t0 = __builtin_fma(-(y0 * 0.25), s0, 0.75);
-  const double t1 = __builtin_fma(-(y1 * 0.25), s1, 0.75);
-  h0 = __builtin_fma(s0, t0, a0);
-  h1 = __builtin_fma(s1, t1, a1);
+  const double t0 = __builtin_fma(-(y0 * 0.5), s0, 1.5);
+  const double t1 = __builtin_fma(-(y1 * 0.5), s1, 1.5);
+  const double h0 = __builtin_fma(s0, t0, e0);
+  const double h1 = __builtin_fma(s1, t1, e1);
+  u0 = __builtin_fma(h0, 0.5, m0);
+  u1 = __builtin_fma(h1, 0.5, m1);
 }
 
 // One cell of the reference update (:504-537) against the image.  Preconditions
@@ -293,9 +307,10 @@ __device__ __forceinline__ double update_value(double tx_, double ty_, double f)
   const double m = minnn(tx_, ty_);
   if (!(f < dinf()) || !(m < dinf())) return m + f;  // outside the kernel's fast path
   const double dd = tx_ - ty_;
+  if (MODE == 2)  // rb_update2's default candidate, both branches
+    return cand_approx(fabs(dd) < f ? fabs(dd) : f, 2.0 * (f * f), m);
   if (fabs(dd) < f) {
     const double r = 2.0 * (f * f) - dd * dd;
-    if (MODE == 2) return m + half_two_sided_approx(dd, 2.0 * (f * f));
     if (MODE == 3) return m + (fabs(dd) + sqrt_cr_fast(__builtin_fma(-dd, dd, 2.0 * (f * f)))) * 0.5;
     if (MODE == 4) return two_sided_approx(ty_, dd, 2.0 * (f * f));
     const double sq = MODE == 1 ? sqrt_cr_fast(r) : sqrt(r);
@@ -741,10 +756,11 @@ __device__ __forceinline__ void rb_update2(const double* p, const double* pn, co
   // pn / ps: the same column in the rows above / below (skewed image rows).
   // All neighbour reads in flight before the first use (cell 1's W is cell 0's E).
   double w0 = p[-1], e0 = p[1], n0 = pn[0], so0 = ps[0];
-  double w1 = p[1], e1 = p[3], n1 = pn[2], so1 = ps[2];
-  // one wait for all of them (the v_min asm below would otherwise pin reads behind it)
-  asm volatile("" : "+v"(w0), "+v"(e0), "+v"(n0), "+v"(so0), "+v"(w1), "+v"(e1), "+v"(n1),
-               "+v"(so1));
+  double e1 = p[3], n1 = pn[2], so1 = ps[2];
+  // one wait for all of them (the v_min asm below would otherwise pin reads behind it);
+  // cell 1's W is cell 0's E, one register (a separate asm operand costs a copy)
+  asm volatile("" : "+v"(w0), "+v"(e0), "+v"(n0), "+v"(so0), "+v"(e1), "+v"(n1), "+v"(so1));
+  const double w1 = e0;
   // No skip test: u < t alone decides (u >= min + C/sqrt(2) > min + 0.7071 C, so
   // the skip test of rb_update never rejects an improving candidate), and the
   // half-sweep is one straight-line dependent chain without a scalar branch.
@@ -754,12 +770,20 @@ __device__ __forceinline__ void rb_update2(const double* p, const double* pn, co
   const double m0 = vmin64(tx0, ty0), m1 = vmin64(tx1, ty1);
   {
     const double d0 = tx0 - ty0, d1 = tx1 - ty1;
-    // the monotone combine (half_two_sided_approx): T' = min + h, h = C on the
-    // one-sided branch; the select comes before the one add at the scale of T
+    // the monotone combine: T' = min + h, h = C on the one-sided branch; the select
+    // (or the clamp of cand_approx) comes before the one add at the scale of T
     double h0, h1;  // two-sided half-sums (|d| + sqrt(2C^2 - d^2)) / 2
     if constexpr (FAST && APPROX) {
-      // an obstacle (f = inf) gives NaN here (rsq(inf) * inf), which v_min ignores
-      half_two_sided_approx2(d0, c20, d1, c21, h0, h1);
+      // cand_approx: the branch folded into the argument min(|d|, C).  An obstacle
+      // (f = inf) gives NaN (rsq(inf) * inf), which v_min ignores; d = NaN (no finite
+      // neighbour) gives min(|NaN|, C) = C, and m = inf keeps the candidate at inf
+      double u0, u1;
+      cand_approx2(vmin64_abs(d0, f0), c20, m0, vmin64_abs(d1, f1), c21, m1, u0, u1);
+      ch0 = u0 < t0;
+      ch1 = u1 < t1;
+      t0 = vmin64(t0, u0);
+      t1 = vmin64(t1, u1);
+      return;
     } else {
       const double r0 = __builtin_fma(-d0, d0, c20), r1 = __builtin_fma(-d1, d1, c21);
       double q0, q1;
