@@ -457,8 +457,8 @@ def main():
             "grid": N,
             # what the headline computes in (DESIGN.md s4 "Sweep sqrt", s3 tolerance)
             "arith": ("fp64, correctly rounded sweep sqrt (DYMU_EXACT_SQRT=1)" if _EXACT else
-                      "fp64, approx sweep sqrt (one Goldschmidt step, <= 36 ulp on the "
-                      "two-sided candidate; solve error vs the reference FMM <= 6e-15 rel)"),
+                      "fp64, approx sweep sqrt (one Goldschmidt step, <= 36 ulp on the sqrt "
+                      "term of each candidate; solve error vs the reference FMM <= 1e-14 rel)"),
             "schedule": "default (sweep deadline + first-insertion histogram: last ulps vary "
                         "run to run)",
             "parallelism": ("single" if world == 1 and not args.sharded else
