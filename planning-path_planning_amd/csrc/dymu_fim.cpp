@@ -351,13 +351,16 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   // also stops sweeping 14 us into the pass (re-queued like a capped one): 46.0 vs
   // 49.2 ms at 16384^2 (v9), 15.6 vs 16.0 ms at 8192^2 (v11).  Whole grids from 2^18
   // tiles; slabs (more exchange rounds with it) only from 2^20.
+  // v33 (13 instead of 16.5 fp64 instructions per update) and the strided entries moved
+  // the optimum for those grids to a cap of 18 and a deadline of 15 us: 28.48-28.54 vs
+  // 29.90 ms at 16384^2, 1,392 vs 1,562 passes (profiles/r04/v34_knobs.txt)
   const bool big = ntiles >= (1u << 20) || (!ghost_lo && !ghost_hi && ntiles >= (1u << 18));
   a.max_inner = c->opts.max_inner > 0 ? c->opts.max_inner
-                : variant == 5            ? 16
+                : variant == 5            ? (big ? 18 : 16)
                                           : 4 * (TWd + THd);
   if (const char* kv = std::getenv("DYMU_MAX_INNER")) a.max_inner = std::max(1, std::atoi(kv));
 
-  a.sweep_deadline = (variant == 5 && big) ? 1400u : 0u;  // 10-ns s_memrealtime ticks
+  a.sweep_deadline = (variant == 5 && big) ? 1500u : 0u;  // 10-ns s_memrealtime ticks
   if (const char* kv = std::getenv("DYMU_SWEEP_DEADLINE"))
     a.sweep_deadline = (uint32_t)std::max(0, std::atoi(kv));
   // at most 90% of the listed tiles per pass: a short list (the serpentine maze, the first

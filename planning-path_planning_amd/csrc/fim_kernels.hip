@@ -1326,16 +1326,19 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   uint32_t my_cd = 0, my_cap = 0, my_dl = 0, my_rmax = 0, my_rmin = ~0u;  // a.pstat only
   double* img = s_img[wv];
   unsigned long long* ek = s_ek[wv];
-  const uint32_t chunk = (n_active + gridDim.x - 1) / gridDim.x;
-  const uint32_t c0 = blockIdx.x * chunk;
-  const uint32_t c1 = min(n_active, c0 + chunk);
+  // the workgroup's entries are every gridDim.x-th of the list from its own index, not
+  // a contiguous chunk: a producer flushes its queue contiguously, so a chunk holds
+  // neighbours of the same visits -- mostly admitted or mostly deferred together -- and
+  // a workgroup with more visits than waves ends the pass late; strided, the visits
+  // per workgroup spread binomially around the mean
+  const uint32_t nb = gridDim.x;
   bool first = true;
   if (trace && tid == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
   for (;;) {  // wave-uniform
     uint32_t e = 0;
-    if (lane == 0) e = c0 + atomicAdd(&s_next, 1u);
+    if (lane == 0) e = blockIdx.x + atomicAdd(&s_next, 1u) * nb;
     e = __builtin_amdgcn_readfirstlane(e);
-    if (e >= c1) break;
+    if (e >= n_active) break;
     const uint32_t ent =
         __builtin_amdgcn_readfirstlane(list_at_wave(a.list_in, a.shard_cap, s_pref, e, lane));
     const uint32_t tile = ent & kTileMask;
@@ -1508,7 +1511,8 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
     a.list_out[(uint64_t)shard * a.shard_cap + s_base + k] = s_q[k];
   if (trace && tid == 0) {
     trace[4] = __builtin_amdgcn_s_memrealtime();
-    trace[5] = ((unsigned long long)(c1 > c0 ? c1 - c0 : 0) << 32) | (unsigned long long)s_visits;
+    const uint32_t mine = n_active > blockIdx.x ? (n_active - blockIdx.x - 1) / nb + 1 : 0u;
+    trace[5] = ((unsigned long long)mine << 32) | (unsigned long long)s_visits;
   }
 }
 
