@@ -813,13 +813,15 @@ template <bool FAST, bool APPROX = false>
 __device__ __forceinline__ int rb_sweeps4(double* pr, double* pb, int dn, int ds,
                                           const double (&fr)[2], const double (&fb)[2],
                                           double (&tr)[2], double (&tb)[2], int max_inner,
-                                          bool& capped, unsigned long long stop_at = ~0ull) {
+                                          bool& capped, uint32_t stop_at) {
   const double *prn = pr + dn, *prs = pr - ds, *pbn = pb + dn, *pbs = pb - ds;
   int sweeps = 0;
   capped = true;
   // past stop_at (the pass deadline) a visit ends as if capped -- but only after
   // its first sweep pair, so every visit makes progress and the solve terminates
-  while (sweeps < max_inner && (sweeps == 0 || __builtin_amdgcn_s_memrealtime() < stop_at)) {
+  // (the low 32 bits of the 10-ns clock, compared wrap-safe: scalar instructions only)
+  while (sweeps < max_inner &&
+         (sweeps == 0 || (int32_t)(stop_at - (uint32_t)__builtin_amdgcn_s_memrealtime()) > 0)) {
     bool i0, i1, i2, i3;
     // two sweeps per convergence test: the second sweep's flags decide (a sweep
     // that changes nothing is the local fixed point)
@@ -841,7 +843,9 @@ __device__ __forceinline__ int rb_sweeps4(double* pr, double* pb, int dn, int ds
     pb[0] = tb[0];
     pb[2] = tb[1];
     ++sweeps;
-    if (!__any(i0 || i1 || i2 || i3)) {
+    // the lane masks of the four compares, or-ed in scalar registers (no VGPR round trip)
+    if ((__builtin_amdgcn_ballot_w64(i0) | __builtin_amdgcn_ballot_w64(i1) |
+         __builtin_amdgcn_ballot_w64(i2) | __builtin_amdgcn_ballot_w64(i3)) == 0) {
       capped = false;
       break;
     }
@@ -859,7 +863,7 @@ struct NoGate {
 template <bool APPROX = false, class Gate = NoGate>
 __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned long long* ek,
                                        bool has, int tx, int ty, int lane, bool& capped,
-                                       Gate gate = Gate(), unsigned long long stop_at = ~0ull) {
+                                       Gate gate, uint32_t stop_at) {
   const int cap = a.max_inner;
   constexpr int TT = 16;
   const int r = lane >> 2, q = lane & 3, odd = r & 1;
@@ -1235,7 +1239,8 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   const uint32_t shard = blockIdx.x % kShards;
   unsigned long long* trace = a.trace ? a.trace + (uint64_t)blockIdx.x * kTracePts : nullptr;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  const unsigned long long stop_at = a.sweep_deadline ? t_start + a.sweep_deadline : ~0ull;
+  // no deadline: 2^30 ticks (10.7 s) ahead, far beyond any pass
+  const uint32_t stop_at = (uint32_t)t_start + (a.sweep_deadline ? a.sweep_deadline : (1u << 30));
   if (trace && tid == 0) trace[0] = t_start;
 
   const double delta = *a.delta;
