@@ -34,12 +34,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec peak
 BYTES_PER_CELL_VISIT = 24  # read T 8 + read F 8 + write T 8
 BYTES_PER_CELL_SOLVE = 16  # read F once + write T once
 # The pass kernel's real limiter is the fp64 VALU (and the latency of its pass chain,
-# DESIGN.md s4), not HBM.  Kernel 5's sweep loop issues 137 VALU instructions per pair
-# of sweeps over a lane's 4 cells (ISA count of the fast path, llvm -S of
-# fim_kernels.hip; 201 with dymu_opts.exact_sqrt = 1, whose candidate takes 8 more per
-# update): 17.1 per cell update.  Peak: MI355X fp64 vector 78.6 TFLOP/s =
+# DESIGN.md s4), not HBM.  Kernel 5's sweep loop issues 108 VALU instructions per pair
+# of sweeps over a lane's 4 cells (ISA count of the fast path at v35, llvm-objdump of
+# fim_kernels.hip; v32: 137): 13.5 per cell update, one of them v_rsq_f64 (issue cost
+# ~3x a plain fp64 op, tools/valu_probe.hip).  Peak: MI355X fp64 vector 78.6 TFLOP/s =
 # 256 CUs x 4 SIMDs x 16 lanes x 2.4 GHz = 39.3 T lane-instructions/s.
-VALU_PER_CELL_UPDATE = {5: 137 / 8}
+VALU_PER_CELL_UPDATE = {5: 108 / 8}
 VALU_PEAK_T = 256 * 4 * 16 * 2.4e9 / 1e12
 
 
