@@ -150,10 +150,10 @@ class DyMuPathPlanner {
   bool isFullyClosedNode(unsigned i, unsigned j);  // :424-436 (border -> false)
   void resetTotalCostMap();                        // :473-485: every node OPEN at +inf
   // the reference's global_narrowband (:445) as the last computeTotalCostMap left
-  // it: snapshots of the band nodes in grid-index order (the reference keeps
-  // insertion order); empty after computeEntireTotalCostMap
+  // it: snapshots of the band nodes in the reference's insertion order (rebuilt from
+  // the values, csrc/pop_order.hpp); empty after computeEntireTotalCostMap
   std::vector<globalNode> globalNarrowband();
-  // :548-567: the band node with the lowest total cost (first in grid-index order
+  // :548-567: the band node with the lowest total cost (first in insertion order
   // on ties), removed from the band list like the reference's erase; the map is
   // not changed.  std::nullopt on an empty band (the reference reads front()).
   std::optional<globalNode> minCostGlobalNode();
@@ -267,6 +267,16 @@ class DyMuPathPlanner {
                                const double* tr);
   // Narrow-band cells left by the last computeTotalCostMap (0 after a full solve).
   uint64_t lastBandSize() const { return band_cells_.size(); }
+  // How the last computeTotalCostMap resolved the reference's order at its exit
+  // value: cells of exactly that value, how many of them the
+  // reference had not closed yet, whether the exact host replay ran (degenerate
+  // ties only), host time of the resolution and band replay.
+  struct EarlyExitInfo {
+    uint64_t tied = 0, open_at_limit = 0;
+    int exact_replay = 0;
+    double resolve_ms = 0.0;
+  };
+  const EarlyExitInfo& lastEarlyExitInfo() const { return early_info_; }
   // Engine options (device ordinal etc.); takes effect on the next solve.
   void setEngineOptions(const dymu_opts& o);
   // Install a total-cost map (ny*nx, +inf unreachable) as the state a
@@ -314,10 +324,14 @@ class DyMuPathPlanner {
   template <class ERows, class TRows>
   bool costMapFromRows(const ERows& elev_row, const TRows& terr_row);
   bool propagate(bool early, unsigned si, unsigned sj);
-  // returns true when the replay met equal values whose pop order decides the result
-  bool replayBand(double t_closed, const std::vector<uint64_t>& band, std::vector<double>& out);
-  // the reference's early exit replayed exactly on the host (ties at the exit)
+  // the band's tentative values at the moment `last` was popped; true when the
+  // reference's pop order was undetermined (degenerate ties): out is then unusable
+  bool replayBand(uint64_t last, const std::vector<uint64_t>& band, std::vector<double>& out);
+  // the reference's early exit replayed exactly on the host (degenerate ties only)
   bool exactEarlyExit(unsigned si, unsigned sj);
+  static constexpr uint64_t kExactReplayCells = 1ull << 24;
+  // band_cells_ into the reference's insertion order, if still in grid order
+  void orderBand();
   bool safeNode(unsigned i, unsigned j) const;
   std::optional<globalNode> snapshot(uint64_t k);
   void nominalCost(unsigned i, unsigned j, int range, int num_locs, double cmax);
@@ -371,8 +385,13 @@ class DyMuPathPlanner {
   mutable uint64_t blk_missing_ = 0;
   unsigned nbx_ = 0, nby_ = 0;
   void* registered_ = nullptr;  // total_cost_ buffer page-locked for DMA
-  double closed_limit_ = 0.0;   // CLOSED iff finite T <= closed_limit_
-  std::vector<uint64_t> band_cells_;  // global_narrowband: grid indices, ascending
+  double closed_limit_ = 0.0;   // CLOSED iff finite T <= closed_limit_ ...
+  // ... except these cells of exactly closed_limit_ (sorted): the reference's early
+  // exit came before it popped them
+  std::vector<uint64_t> open_at_limit_;
+  std::vector<uint64_t> band_cells_;  // global_narrowband: grid indices
+  bool band_unordered_ = false;       // band_cells_ in grid order until orderBand()
+  EarlyExitInfo early_info_{};
   // F as uploaded to dF_ (host copy); node-field rows [dirty_j0_, dirty_j1_)
   // changed since it was packed
   std::vector<double> speed_;

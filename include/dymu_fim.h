@@ -137,6 +137,11 @@ int dymu_early_exit_mask(dymu_ctx* ctx, const double* dF, double* dT, uint32_t n
  * Synchronises `stream`. */
 int dymu_count_equal(dymu_ctx* ctx, const double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
                      double value, uint64_t* count, void* stream);
+/* dymu_count_equal that also lists the cells: *count = their number, idx (host,
+ * cap entries) their indices j*nx + i (the first cap found, unordered).  The
+ * planner's early exit resolves the reference's order among them. */
+int dymu_find_equal(dymu_ctx* ctx, const double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
+                    double value, uint64_t* idx, uint64_t cap, uint64_t* count, void* stream);
 /* dT[(idx[k] / nx) * ld + idx[k] % nx] = vals[k] for k < n (idx, vals: host). */
 int dymu_scatter(dymu_ctx* ctx, double* dT, uint32_t nx, uint64_t ld, const uint64_t* idx,
                  const double* vals, uint64_t n, void* stream);

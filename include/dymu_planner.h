@@ -76,6 +76,10 @@ int dymu_planner_set_trafficability_window(dymu_planner* p, uint32_t i0, uint32_
 int64_t dymu_planner_last_band_size(dymu_planner* p);
 /* statistics of the last solve */
 int dymu_planner_last_stats(dymu_planner* p, dymu_stats* out);
+/* the last computeTotalCostMap's exit-order resolution: out[0] cells
+ * of exactly the exit value, out[1] how many of them the reference had not closed,
+ * out[2] 1 if the exact host replay ran (degenerate ties only), out[3] host ms */
+int dymu_planner_last_early_exit(dymu_planner* p, double out[4]);
 /* how the last solve ran: 0 cold, 1 windowed re-propagation from the window
  * where the speed changed (dymu_resolve_window), 2 previous map reused */
 int dymu_planner_last_solve_kind(dymu_planner* p);
@@ -94,7 +98,7 @@ int dymu_planner_is_safe_node(dymu_planner* p, uint32_t i, uint32_t j);         
 int dymu_planner_is_fully_closed_node(dymu_planner* p, uint32_t i, uint32_t j);  /* :424-436 */
 int dymu_planner_reset_total_cost_map(dymu_planner* p);                          /* :473-485 */
 /* global_narrowband (:445) as the last computeTotalCostMap left it: the band
- * size; up to max (i, j) pairs written to ij in grid-index order */
+ * size; up to max (i, j) pairs written to ij in the reference's insertion order */
 int64_t dymu_planner_global_narrowband(dymu_planner* p, uint32_t* ij, int64_t max);
 /* minCostGlobalNode (:548-567): 1, the band node of lowest total cost (removed
  * from the band list) in ij[2] and *total_cost; 0 on an empty band */

@@ -389,16 +389,17 @@ static hent_t hpop(heap_t* h) {
   return top;
 }
 
-int oracle_fmm_heap(const double* F, uint32_t nx, uint32_t ny, uint32_t gi, uint32_t gj,
+static int fmm_heap(const double* F, uint32_t nx, uint32_t ny, uint32_t gi, uint32_t gj,
                     int64_t start_i, int64_t start_j, double* T, uint8_t* closed,
-                    uint64_t* n_pops) {
+                    uint64_t* n_pops, uint64_t* seq_out) {
   if (!check_args(nx, ny, gi, gj, start_i, start_j)) return -1;
   const uint64_t n = (uint64_t)nx * ny;
   uint8_t* cl = closed ? closed : (uint8_t*)malloc(n);
-  uint64_t* seq = (uint64_t*)malloc(sizeof(uint64_t) * n);
+  uint64_t* seq = seq_out ? seq_out : (uint64_t*)malloc(sizeof(uint64_t) * n);
   for (uint64_t k = 0; k < n; ++k) {
     T[k] = INF_D;
     cl[k] = 0;
+    seq[k] = UINT64_MAX;
   }
   const int early = start_i >= 0;
   const uint64_t s = early ? (uint64_t)start_j * nx + (uint64_t)start_i : 0;
@@ -441,9 +442,24 @@ int oracle_fmm_heap(const double* F, uint32_t nx, uint32_t ny, uint32_t gi, uint
   }
   if (n_pops) *n_pops = pops;
   free(h.v);
-  free(seq);
+  if (!seq_out) free(seq);
   if (!closed) free(cl);
   return live > 0 ? 1 : 0;
+}
+
+int oracle_fmm_heap(const double* F, uint32_t nx, uint32_t ny, uint32_t gi, uint32_t gj,
+                    int64_t start_i, int64_t start_j, double* T, uint8_t* closed,
+                    uint64_t* n_pops) {
+  return fmm_heap(F, nx, ny, gi, gj, start_i, start_j, T, closed, n_pops, NULL);
+}
+
+/* The same FMM, also returning each node's band-insertion sequence number (the
+ * position it takes in global_narrowband / global_propagated_nodes when it first
+ * becomes finite, :537-545; the goal 0, :487-498; UINT64_MAX never reached). */
+int oracle_fmm_order(const double* F, uint32_t nx, uint32_t ny, uint32_t gi, uint32_t gj,
+                     int64_t start_i, int64_t start_j, double* T, uint8_t* closed,
+                     uint64_t* seq) {
+  return fmm_heap(F, nx, ny, gi, gj, start_i, start_j, T, closed, NULL, seq);
 }
 
 /* ------------------------------------------------------------------ */

@@ -85,6 +85,12 @@ int oracle_fmm_linear(const double* F, uint32_t nx, uint32_t ny, uint32_t gi, ui
 int oracle_fmm_heap(const double* F, uint32_t nx, uint32_t ny, uint32_t gi, uint32_t gj,
                     int64_t start_i, int64_t start_j, double* T, uint8_t* closed,
                     uint64_t* n_pops);
+/* oracle_fmm_heap plus each node's band-insertion sequence number seq[k] (its
+ * position in the reference's global_narrowband / global_propagated_nodes when it
+ * first became finite; goal 0; UINT64_MAX never reached). */
+int oracle_fmm_order(const double* F, uint32_t nx, uint32_t ny, uint32_t gi, uint32_t gj,
+                     int64_t start_i, int64_t start_j, double* T, uint8_t* closed,
+                     uint64_t* seq);
 
 /* All-cores CPU baseline (oracle_par.c, SURVEY s8(d) cpu_fim_omp): the same fixed
  * point reached by a block FIM over `threads` OpenMP threads (64 x 64 tiles, a

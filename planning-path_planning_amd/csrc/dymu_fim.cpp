@@ -1272,9 +1272,32 @@ int dymu_count_equal(dymu_ctx* c, const double* dT, uint32_t nx, uint32_t ny, ui
   hipStream_t st = pick_stream(c, stream);
   unsigned long long* cnt = c->d_scratch + 4;
   HIPC(c, hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
-  HIPC(c, launch_count_equal(dT, (int64_t)ld, nx, ny, value, cnt, st));
+  HIPC(c, launch_count_equal(dT, (int64_t)ld, nx, ny, value, cnt, nullptr, 0, st));
   HIPC(c, hipMemcpyAsync(c->h_probe, cnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   HIPC(c, hipStreamSynchronize(st));
+  *count = c->h_probe[0];
+  return DYMU_OK;
+}
+
+int dymu_find_equal(dymu_ctx* c, const double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
+                    double value, uint64_t* idx, uint64_t cap, uint64_t* count, void* stream) {
+  if (!c || !dT || !count || ld < nx || (cap && !idx)) return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  hipStream_t st = pick_stream(c, stream);
+  unsigned long long* cnt = c->d_scratch + 4;
+  uint64_t* di = nullptr;
+  const uint64_t dcap = cap ? cap : 1;
+  HIPC(c, hipMallocAsync(reinterpret_cast<void**>(&di), sizeof(uint64_t) * dcap, st));
+  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st);
+  if (e == hipSuccess) e = launch_count_equal(dT, (int64_t)ld, nx, ny, value, cnt, di, cap, st);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(c->h_probe, cnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  const uint64_t m = e == hipSuccess ? std::min<uint64_t>(c->h_probe[0], cap) : 0;
+  if (m) e = hipMemcpy(idx, di, sizeof(uint64_t) * m, hipMemcpyDeviceToHost);
+  (void)hipFreeAsync(di, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return fail_hip(c, e, "dymu_find_equal");
   *count = c->h_probe[0];
   return DYMU_OK;
 }

@@ -235,9 +235,11 @@ struct UpdateArgs {
 hipError_t launch_window_min(const double* T, int64_t ld, uint32_t i0, uint32_t j0, uint32_t i1,
                              uint32_t j1, unsigned long long* out, hipStream_t st);
 hipError_t launch_reset_seed(const UpdateArgs& a, hipStream_t st);
-// *out += the number of cells of T (nx x ny, pitch ld) whose bits equal value's
+// *out += the number of cells of T (nx x ny, pitch ld) whose bits equal value's;
+// with idx (device, cap entries) also the first cap of their indices j*nx + i
 hipError_t launch_count_equal(const double* T, int64_t ld, uint32_t nx, uint32_t ny, double value,
-                              unsigned long long* out, hipStream_t st);
+                              unsigned long long* out, uint64_t* idx, uint64_t cap,
+                              hipStream_t st);
 // decrease-only window [i0,i1) x [j0,j1): seed the tiles that intersect it, no reset
 hipError_t launch_seed_window(const UpdateArgs& a, uint32_t i0, uint32_t j0, uint32_t i1,
                               uint32_t j1, hipStream_t st);

@@ -11,6 +11,7 @@
 //     on first read (path extraction reads a narrow band around the path) or
 //     all of it for the matrix getters.
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <cmath>
@@ -24,6 +25,7 @@
 
 #include "DyMu.hpp"
 #include "local_layer.hpp"
+#include "pop_order.hpp"
 
 namespace PathPlanning_lib {
 
@@ -113,6 +115,8 @@ bool DyMuPathPlanner::initGlobalLayer(double globalres, double localres, unsigne
   blk_missing_ = 0;
   closed_limit_ = 0.0;
   band_cells_.clear();
+  band_unordered_ = false;
+  open_at_limit_.clear();
   node_state_.clear();
   propagated_extra_.clear();
   manual_list_ = false;
@@ -644,7 +648,9 @@ void DyMuPathPlanner::copyTotalCost(double* out, bool raw) const {
 bool DyMuPathPlanner::closedCell(uint64_t k) const {
   if (!node_state_.empty()) return node_state_[k] != 0;
   const double t = T(k);
-  return t < kInf && t <= closed_limit_;
+  if (!(t < kInf) || t > closed_limit_) return false;
+  return t < closed_limit_ || open_at_limit_.empty() ||
+         !std::binary_search(open_at_limit_.begin(), open_at_limit_.end(), k);
 }
 
 // One propagation on the engine.  early = computeTotalCostMap (:364-408): stop
@@ -691,9 +697,12 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
   std::fill(blk_ok_.begin(), blk_ok_.end(), 0);
   blk_missing_ = blk_ok_.size();
   band_cells_.clear();
+  band_unordered_ = false;
+  open_at_limit_.clear();
   node_state_.clear();
   propagated_extra_.clear();
   manual_list_ = false;
+  early_info_ = EarlyExitInfo{};
   if (!early) {
     closed_limit_ = kInf;
     solved_ = true;
@@ -718,69 +727,158 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
   }
   band.resize(nb);
   std::sort(band.begin(), band.end());
-  // exact ties decide the reference's CLOSED set (cells of exactly t_closed besides the
-  // last one it closes) or a band value (the replay met equal values): replay the
-  // reference exactly on the host instead
-  uint64_t at_t = 0;
-  if (t_closed < kInf &&
-      dymu_count_equal(ctx_, dT_, nx_, ny_, nx_, t_closed, &at_t, nullptr) != DYMU_OK)
-    throw std::runtime_error(std::string("dymu_count_equal failed: ") + dymu_last_error(ctx_));
-  if (at_t > 1) return exactEarlyExit(si, sj);
-  if (nb) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint64_t g = idx(goal_i_, goal_j_), s = idx(si, sj);
+  auto mirror = [this](uint64_t k) { return T(k); };
+  PopOrder<decltype(mirror)> po(mirror, nx_, ny_, g);
+  // Cells of exactly t_closed: the reference pops them in insertion order and stops
+  // right after the last of the start and its nb4, so those it pops later stay in
+  // the band (with their value).  Resolve which, from the values (pop_order.hpp).
+  if (t_closed < kInf) {
+    std::vector<uint64_t> eq(256);
+    uint64_t n_eq = 0;
+    for (;;) {
+      if (dymu_find_equal(ctx_, dT_, nx_, ny_, nx_, t_closed, eq.data(), eq.size(), &n_eq,
+                          nullptr) != DYMU_OK)
+        throw std::runtime_error(std::string("dymu_find_equal failed: ") + dymu_last_error(ctx_));
+      if (n_eq <= eq.size()) break;
+      eq.resize(n_eq);
+    }
+    eq.resize(n_eq);
+    early_info_.tied = n_eq;
+    if (n_eq > 1) {
+      const uint64_t probes[5] = {s, s - nx_, s - 1, s + 1, s + nx_};
+      uint64_t last = s;
+      bool have = false;
+      for (const uint64_t q : probes)
+        if (T(q) == t_closed && (!have || po.popBefore(last, q))) {
+          last = q;
+          have = true;
+        }
+      for (const uint64_t x : eq)
+        if (x != last && po.popBefore(last, x)) open_at_limit_.push_back(x);
+      std::sort(open_at_limit_.begin(), open_at_limit_.end());
+    }
+  }
+  // the band with the cells the reference left OPEN at t_closed: they join it, and
+  // a neighbour of theirs stays in it only if it has another CLOSED neighbour
+  // (otherwise it was never reached: +inf)
+  std::vector<uint64_t> unreached;
+  if (!open_at_limit_.empty()) {
+    std::vector<uint64_t> add(open_at_limit_);
+    for (const uint64_t x : open_at_limit_) {
+      const unsigned i = (unsigned)(x % nx_), j = (unsigned)(x / nx_);
+      const int64_t nb4[4][2] = {{i, (int64_t)j - 1}, {(int64_t)i - 1, j}, {i + 1, j}, {i, j + 1}};
+      for (const auto& q : nb4) {
+        if (q[0] < 0 || q[1] < 0 || q[0] >= nx_ || q[1] >= ny_) continue;
+        const uint64_t y = idx((unsigned)q[0], (unsigned)q[1]);
+        if (!std::binary_search(band.begin(), band.end(), y) || T(y) <= t_closed) continue;
+        bool reached = false;
+        const unsigned yi = (unsigned)q[0], yj = (unsigned)q[1];
+        if (yj > 0) reached |= closedCell(y - nx_);
+        if (yi > 0) reached |= closedCell(y - 1);
+        if (yi + 1 < nx_) reached |= closedCell(y + 1);
+        if (yj + 1 < ny_) reached |= closedCell(y + nx_);
+        if (!reached) unreached.push_back(y);
+      }
+    }
+    std::sort(unreached.begin(), unreached.end());
+    unreached.erase(std::unique(unreached.begin(), unreached.end()), unreached.end());
+    std::vector<uint64_t> kept;
+    kept.reserve(band.size() + add.size());
+    for (const uint64_t y : band)
+      if (!std::binary_search(unreached.begin(), unreached.end(), y)) kept.push_back(y);
+    kept.insert(kept.end(), add.begin(), add.end());
+    std::sort(kept.begin(), kept.end());
+    band.swap(kept);
+    nb = band.size();
+    if (!unreached.empty()) {
+      const std::vector<double> inf(unreached.size(), kInf);
+      if (dymu_scatter(ctx_, dT_, nx_, nx_, unreached.data(), inf.data(), unreached.size(),
+                       nullptr) != DYMU_OK)
+        throw std::runtime_error(std::string("dymu_scatter failed: ") + dymu_last_error(ctx_));
+      for (const uint64_t y : unreached) {
+        (void)T(y);
+        total_cost_[y] = kInf;
+      }
+    }
+  }
+  early_info_.open_at_limit = open_at_limit_.size();
+  bool degenerate = po.degenerate();
+  if (nb && !degenerate) {
     std::vector<double> vals;
-    if (replayBand(t_closed, band, vals)) return exactEarlyExit(si, sj);
-    rc = dymu_scatter(ctx_, dT_, nx_, nx_, band.data(), vals.data(), nb, nullptr);
-    if (rc != DYMU_OK)
-      throw std::runtime_error(std::string("dymu_scatter failed: ") + dymu_last_error(ctx_));
-    // blocks fetched during the replay hold the pre-replay band values
-    for (uint64_t q = 0; q < nb; ++q) total_cost_[band[q]] = vals[q];
+    uint64_t last = s;
+    for (const uint64_t q : {s - nx_, s - 1, s + 1, s + nx_})
+      if (closedCell(q) && po.popBefore(last, q)) last = q;
+    degenerate = replayBand(last, band, vals);
+    if (!degenerate) {
+      rc = dymu_scatter(ctx_, dT_, nx_, nx_, band.data(), vals.data(), nb, nullptr);
+      if (rc != DYMU_OK)
+        throw std::runtime_error(std::string("dymu_scatter failed: ") + dymu_last_error(ctx_));
+      // blocks fetched during the replay hold the pre-replay band values
+      for (uint64_t q = 0; q < nb; ++q) total_cost_[band[q]] = vals[q];
+    }
+  }
+  early_info_.resolve_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (degenerate) {
+    // a node whose least neighbour has its own value (speeds below the rounding of
+    // the total cost): the values do not determine the reference's order.  Replay
+    // the reference exactly on the host, up to kExactReplayCells; beyond that keep
+    // the engine's state (every cell of exactly t_closed CLOSED) and say so.
+    if ((uint64_t)nx_ * ny_ <= kExactReplayCells) {
+      early_info_.exact_replay = 1;
+      return exactEarlyExit(si, sj);
+    }
+    log_warn("computeTotalCostMap: degenerate ties at the exit value; the pop order among "
+             "them is not reproduced (grid larger than the exact-replay limit)");
+    open_at_limit_.clear();
   }
   band_cells_ = std::move(band);
+  band_unordered_ = band_cells_.size() > 1;
   return nb > 0;
 }
 
 // The reference's tentative band values at its early exit, from the CLOSED
-// values.  FMM pops in increasing T (the CLOSED cells, T <= t_closed, are popped
-// in the order of their values), and each pop of a node c updates its OPEN
-// nb4 x from the values x's neighbours hold at that moment (:462-465, :500-546).
-// So x's value just after all pops up to time t is
-//   val(x, t) = min over CLOSED nb4 c of x with T(c) <= t of cand(x, T(c)),
-// where cand(x, te) is the update with each neighbour n at its value at te: T(n)
-// if n is CLOSED with T(n) <= te, else val(n, te) (n is OPEN then; no pop at te
-// other than c touches n: the grid is bipartite).  An OPEN value at te is >= te
-// >= any CLOSED value at te (the FMM invariant), so an axis with a CLOSED side
-// takes that side and recursion only follows axes whose both sides are OPEN --
-// cells next to the front, at strictly earlier pops.  Ties between equal T
-// values (the reference's insertion order) are not reproduced.
-bool DyMuPathPlanner::replayBand(double t_closed, const std::vector<uint64_t>& band,
+// values.  A pop of node m updates its OPEN nb4 x from the values x's neighbours
+// hold at that moment (:462-465, :500-546), so with "moment c" = just after the pop
+// of node c:
+//   val(x, c) = min over nb4 m of x CLOSED by moment c of cand(x, m),
+// where cand(x, m) is the update with each neighbour n of x at its value at moment
+// m: T(n) if n is CLOSED by then (popped no later than m, in the reference's pop
+// order -- pop_order.hpp -- which decides ties), else val(n, m).  The band values at
+// the exit are val(x, last), last = the last of the start and its nb4 popped.  An
+// OPEN value at moment m is >= T(m) >= any CLOSED value then (the FMM invariant), so
+// an axis with a CLOSED side takes that side and the recursion only follows axes
+// whose two sides are OPEN -- cells next to the front, at strictly earlier pops (x's
+// neighbours are not adjacent to each other).  Returns true when the pop order was
+// undetermined (degenerate ties, pop_order.hpp): the values are not to be used.
+bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& band,
                                  std::vector<double>& out) {
   struct KeyHash {
-    size_t operator()(const std::pair<uint64_t, double>& k) const {
-      uint64_t b;
-      std::memcpy(&b, &k.second, sizeof b);
-      return std::hash<uint64_t>()(k.first * 0x9E3779B97F4A7C15ull ^ b);
+    size_t operator()(const std::pair<uint64_t, uint64_t>& k) const {
+      return std::hash<uint64_t>()(k.first * 0x9E3779B97F4A7C15ull ^ k.second);
     }
   };
+  auto mirror = [this](uint64_t k) { return T(k); };
+  using Order = PopOrder<decltype(mirror)>;
   struct Replay {
-    const DyMuPathPlanner& pl;
+    DyMuPathPlanner& pl;
+    Order po;
     const double* F;
-    double t_closed;
     int64_t NX, NY;
-    std::unordered_map<std::pair<uint64_t, double>, double, KeyHash> memo;
-    // the popped cell whose update is being replayed, and whether a cell of exactly
-    // its value was met: then the reference's insertion order (which of the equal
-    // cells it popped first) decides the value, and the caller replays exactly
-    int64_t cur = -1;
-    bool tie = false;
+    std::unordered_map<std::pair<uint64_t, uint64_t>, double, KeyHash> memo;
 
     bool in_grid(int64_t i, int64_t j) const { return i >= 0 && j >= 0 && i < NX && j < NY; }
-    // value of a cell CLOSED at (pop) time te, else +inf
-    double closed_val(int64_t i, int64_t j, double te) {
+    // value of (i, j) if it is CLOSED by moment c, else +inf
+    double closed_by(int64_t i, int64_t j, uint64_t c) {
       if (!in_grid(i, j)) return kInf;
-      const int64_t k = j * NX + i;
-      const double t = pl.T((uint64_t)k);
-      if (t == te && t <= t_closed && k != cur) tie = true;
-      return (t <= t_closed && t <= te) ? t : kInf;
+      const uint64_t k = (uint64_t)(j * NX + i);
+      if (!pl.closedCell(k)) return kInf;
+      const double t = pl.T(k), tc = pl.T(c);
+      if (t < tc || k == c) return t;
+      if (t > tc) return kInf;
+      return po.popBefore(k, c) ? t : kInf;
     }
     // the reference update (:504-535), -ffp-contract=off
     static double eikonal(double tx, double ty, double C) {
@@ -788,46 +886,52 @@ bool DyMuPathPlanner::replayBand(double t_closed, const std::vector<uint64_t>& b
         return (tx + ty + std::sqrt(2 * (C * C) - (tx - ty) * (tx - ty))) / 2;
       return std::fmin(tx, ty) + C;
     }
-    double axis(int64_t ia, int64_t ja, int64_t ib, int64_t jb, double te, int depth) {
-      const double a = closed_val(ia, ja, te), b = closed_val(ib, jb, te);
-      if (a < kInf || b < kInf) return std::fmin(a, b);  // OPEN sides are >= te >= it
-      const double va = in_grid(ia, ja) ? val((uint64_t)ja * NX + ia, te, depth + 1) : kInf;
-      const double vb = in_grid(ib, jb) ? val((uint64_t)jb * NX + ib, te, depth + 1) : kInf;
+    double axis(int64_t ia, int64_t ja, int64_t ib, int64_t jb, uint64_t m, int depth) {
+      const double a = closed_by(ia, ja, m), b = closed_by(ib, jb, m);
+      if (a < kInf || b < kInf) return std::fmin(a, b);  // OPEN sides are >= T(m) >= it
+      const double va = in_grid(ia, ja) ? val((uint64_t)(ja * NX + ia), m, depth + 1) : kInf;
+      const double vb = in_grid(ib, jb) ? val((uint64_t)(jb * NX + ib), m, depth + 1) : kInf;
       return std::fmin(va, vb);
     }
-    double val(uint64_t k, double t, int depth) {
+    double val(uint64_t k, uint64_t c, int depth) {
       const double C = F[k];
       if (!(C < kInf)) return kInf;       // obstacles are never updated
       if (depth > 20000) return pl.T(k);  // pathological chains: the converged value
-      const auto key = std::make_pair(k, t);
+      const auto key = std::make_pair(k, c);
       auto it = memo.find(key);
       if (it != memo.end()) return it->second;
-      // in progress: a tie cycle (two OPEN cells each reached through a CLOSED
-      // neighbour of exactly equal T) reads +inf here instead of recursing
       memo.emplace(key, kInf);
       const int64_t i = (int64_t)(k % NX), j = (int64_t)(k / NX);
       double v = kInf;
       const int64_t nb[4][2] = {{i, j - 1}, {i - 1, j}, {i + 1, j}, {i, j + 1}};
       for (const auto& e : nb) {
-        const int64_t saved = cur;
-        cur = in_grid(e[0], e[1]) ? e[1] * NX + e[0] : -1;
-        const double te = closed_val(e[0], e[1], t);
-        if (!(te < kInf)) {  // not CLOSED by time t: no pop of it updated x yet
-          cur = saved;
-          continue;
-        }
-        const double tx = axis(i - 1, j, i + 1, j, te, depth);
-        const double ty = axis(i, j - 1, i, j + 1, te, depth);
-        cur = saved;
+        if (!(closed_by(e[0], e[1], c) < kInf)) continue;  // no pop of it updated k yet
+        const uint64_t m = (uint64_t)(e[1] * NX + e[0]);
+        const double tx = axis(i - 1, j, i + 1, j, m, depth);
+        const double ty = axis(i, j - 1, i, j + 1, m, depth);
         v = std::fmin(v, eikonal(tx, ty, C));
       }
       memo[key] = v;
       return v;
     }
-  } rec{*this, speed_.data(), t_closed, (int64_t)nx_, (int64_t)ny_, {}};
+  } rec{*this, Order(mirror, nx_, ny_, idx(goal_i_, goal_j_)), speed_.data(), (int64_t)nx_,
+        (int64_t)ny_, {}};
   out.resize(band.size());
-  for (size_t q = 0; q < band.size(); ++q) out[q] = rec.val(band[q], t_closed, 0);
-  return rec.tie;
+  for (size_t q = 0; q < band.size(); ++q) out[q] = rec.val(band[q], last, 0);
+  return rec.po.degenerate();
+}
+
+// band_cells_ after a GPU early exit are in grid order: put them in the reference's
+// insertion order (pop_order.hpp) before anyone reads the order
+void DyMuPathPlanner::orderBand() {
+  if (!band_unordered_) return;
+  band_unordered_ = false;
+  auto mirror = [this](uint64_t k) { return T(k); };
+  PopOrder<decltype(mirror)> po(mirror, nx_, ny_, idx(goal_i_, goal_j_));
+  std::vector<uint64_t> b(band_cells_);
+  std::stable_sort(b.begin(), b.end(),
+                   [&po](uint64_t x, uint64_t y) { return po.insBefore(x, y); });
+  if (!po.degenerate()) band_cells_.swap(b);  // else keep grid order
 }
 
 // computeTotalCostMap (:364-408) replayed exactly on the host: the reference FMM with
@@ -911,6 +1015,8 @@ bool DyMuPathPlanner::exactEarlyExit(unsigned si, unsigned sj) {
                              dymu_last_error(ctx_));
   node_state_.swap(closed);
   band_cells_.clear();
+  band_unordered_ = false;
+  open_at_limit_.clear();
   for (const uint64_t k : order)
     if (in_band[k]) band_cells_.push_back(k);  // the reference's band vector, in order
   propagated_extra_.swap(order);
@@ -1229,6 +1335,8 @@ void DyMuPathPlanner::resetTotalCostMap() {
   blk_missing_ = 0;
   closed_limit_ = 0.0;
   band_cells_.clear();
+  band_unordered_ = false;
+  open_at_limit_.clear();
   node_state_.assign(total_cost_.size(), 0);
   propagated_extra_.clear();
   manual_list_ = true;
@@ -1254,6 +1362,7 @@ void DyMuPathPlanner::setGlobalNodeState(unsigned i, unsigned j, node_state s) {
 // of device blocks can overwrite what this writes)
 void DyMuPathPlanner::propagateGlobalNode(unsigned i, unsigned j) {
   if (i >= nx_ || j >= ny_) return;
+  orderBand();  // from the solve's values, before this changes any
   fetchAll();
   const uint64_t k = idx(i, j);
   const double* t = total_cost_.data();
@@ -1321,6 +1430,7 @@ std::vector<globalNode> DyMuPathPlanner::globalPropagatedNodes() {
 }
 
 std::vector<globalNode> DyMuPathPlanner::globalNarrowband() {
+  orderBand();
   std::vector<globalNode> out;
   out.reserve(band_cells_.size());
   for (const uint64_t k : band_cells_) out.push_back(*snapshot(k));
@@ -1330,6 +1440,7 @@ std::vector<globalNode> DyMuPathPlanner::globalNarrowband() {
 // :548-567 (first strict minimum, then erased from the band)
 std::optional<globalNode> DyMuPathPlanner::minCostGlobalNode() {
   if (band_cells_.empty()) return std::nullopt;
+  orderBand();
   size_t best = 0;
   double tmin = T(band_cells_[0]);
   for (size_t q = 1; q < band_cells_.size(); ++q) {
@@ -1347,6 +1458,7 @@ std::optional<globalNode> DyMuPathPlanner::minCostGlobalNode() {
 // :487-498
 void DyMuPathPlanner::resetGlobalNarrowBand() {
   band_cells_.clear();
+  band_unordered_ = false;
   if (!has_goal_ || nx_ == 0) return;
   const uint64_t k = idx(goal_i_, goal_j_);
   (void)T(k);  // the goal's block in the host mirror before the write
@@ -1363,6 +1475,8 @@ bool DyMuPathPlanner::loadTotalCostMap(const double* Tin) {
   blk_missing_ = 0;
   closed_limit_ = kInf;
   band_cells_.clear();
+  band_unordered_ = false;
+  open_at_limit_.clear();
   node_state_.clear();
   propagated_extra_.clear();
   manual_list_ = false;

@@ -203,6 +203,16 @@ int dymu_planner_last_stats(dymu_planner* p, dymu_stats* out) {
   return DYMU_OK;
 }
 
+int dymu_planner_last_early_exit(dymu_planner* p, double out[4]) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  const auto& e = p->pl.lastEarlyExitInfo();
+  out[0] = (double)e.tied;
+  out[1] = (double)e.open_at_limit;
+  out[2] = (double)e.exact_replay;
+  out[3] = e.resolve_ms;
+  return DYMU_OK;
+}
+
 int dymu_planner_last_solve_kind(dymu_planner* p) {
   if (!p) return DYMU_ERR_ARG;
   return p->pl.lastSolveKind();

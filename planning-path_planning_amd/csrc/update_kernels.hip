@@ -52,14 +52,24 @@ __global__ void k_window_min(const double* T, int64_t ld, uint32_t i0, uint32_t 
   if (threadIdx.x == 0 && s_min != kInfBits) atomicMin(out, s_min);
 }
 
-// number of cells whose value is bitwise `value` (early-exit tie detection)
+// number of cells whose value is bitwise `value` (early-exit tie detection); with
+// idx, also their indices j*nx + i (the first cap of them, in no particular order)
 __global__ void k_count_equal(const double* T, int64_t ld, uint32_t nx, uint32_t ny,
-                              unsigned long long vbits, unsigned long long* out) {
+                              unsigned long long vbits, unsigned long long* out, uint64_t* idx,
+                              uint64_t cap) {
   const uint64_t n = (uint64_t)nx * ny;
   unsigned long long c = 0;
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
-       k += (uint64_t)gridDim.x * blockDim.x)
-    c += dbits(T[(int64_t)(k / nx) * ld + (int64_t)(k % nx)]) == vbits ? 1u : 0u;
+       k += (uint64_t)gridDim.x * blockDim.x) {
+    if (dbits(T[(int64_t)(k / nx) * ld + (int64_t)(k % nx)]) != vbits) continue;
+    if (idx) {  // matches are few: one atomic each
+      const unsigned long long pos = atomicAdd(out, 1ull);
+      if (pos < cap) idx[pos] = k;
+    } else {
+      ++c;
+    }
+  }
+  if (idx) return;
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
 }
@@ -371,12 +381,14 @@ hipError_t launch_window_min(const double* T, int64_t ld, uint32_t i0, uint32_t 
 }
 
 hipError_t launch_count_equal(const double* T, int64_t ld, uint32_t nx, uint32_t ny, double value,
-                              unsigned long long* out, hipStream_t st) {
+                              unsigned long long* out, uint64_t* idx, uint64_t cap,
+                              hipStream_t st) {
   uint64_t b = ((uint64_t)nx * ny + 255) / 256;
   if (b > 4096) b = 4096;
   if (b == 0) b = 1;
   hipLaunchKernelGGL(k_count_equal, dim3((unsigned)b), dim3(256), 0, st, T, ld, nx, ny,
-                     (unsigned long long)__builtin_bit_cast(unsigned long long, value), out);
+                     (unsigned long long)__builtin_bit_cast(unsigned long long, value), out, idx,
+                     cap);
   return hipGetLastError();
 }
 

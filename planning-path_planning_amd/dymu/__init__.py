@@ -127,6 +127,8 @@ FIM_SYMBOLS = {
     "dymu_dom_round_peer": (_i32, [_vp, _u32, _vp, _vp]),
     "dymu_count_equal": (_i32, [_vp, _vp, _u32, _u32, _u64, ctypes.c_double,
                                 ctypes.POINTER(_u64), _vp]),
+    "dymu_find_equal": (_i32, [_vp, _vp, _u32, _u32, _u64, ctypes.c_double, _vp, _u64,
+                               ctypes.POINTER(_u64), _vp]),
     "dymu_dom_post_status": (_i32, [_vp, _vp, _vp, _u32]),
     "dymu_dom_post": (_i32, [_vp, _vp, ctypes.POINTER(_u32)]),
     "dymu_dom_wait_post": (_i32, [_vp, _u32, ctypes.c_double, ctypes.POINTER(ctypes.c_int32),
@@ -462,6 +464,7 @@ PLANNER_SYMBOLS = {
     "dymu_planner_set_trafficability": (_i32, [_vp, _dp]),
     "dymu_planner_last_stats": (_i32, [_vp, ctypes.POINTER(DymuStats)]),
     "dymu_planner_last_solve_kind": (_i32, [_vp]),
+    "dymu_planner_last_early_exit": (_i32, [_vp, _dp]),
     "dymu_planner_set_hazard_density_window": (_i32, [_vp, _u32, _u32, _u32, _u32, _dp]),
     "dymu_planner_set_trafficability_window": (_i32, [_vp, _u32, _u32, _u32, _u32, _dp]),
     "dymu_planner_last_band_size": (ctypes.c_int64, [_vp]),
@@ -684,6 +687,15 @@ class Planner:
     def lastSolveKind(self) -> int:
         """0 cold solve, 1 windowed re-propagation, 2 previous map reused."""
         return _b_int(self._lib.dymu_planner_last_solve_kind(self.h))
+
+    def lastEarlyExit(self) -> dict:
+        """How the last computeTotalCostMap resolved the reference's pop order at its
+        exit value: tied cells, those left OPEN, whether the exact host replay ran
+        (degenerate ties only), host milliseconds of the resolution and band replay."""
+        o = np.zeros(4)
+        _check(self._lib.dymu_planner_last_early_exit(self.h, o))
+        return {"tied": int(o[0]), "open_at_limit": int(o[1]), "exact_replay": bool(o[2]),
+                "resolve_ms": float(o[3])}
 
     def lastStats(self) -> dict:
         st = DymuStats()

@@ -5,6 +5,7 @@
 //   driver fail     the same with HOST_ENGINE_FAIL_D2H set: the readback must throw
 //   driver options  solve, setEngineOptions, then read the map and a path
 //   driver ties     constant cost (every distance tie), computeTotalCostMap's early exit
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -71,36 +72,75 @@ static int compare(const std::vector<std::vector<double>>& M, const std::vector<
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "ok";
   if (mode == "ties") {
-    // constant cost: every axis distance ties with many others (the early exit's
-    // band replay meets equal CLOSED values on both sides of an OPEN pair)
-    const unsigned N = 160, gi = 80, gj = 80;
-    DyMuPathPlanner p(1.0, 2.0, 5.0, CONSERVATIVE);
-    p.initGlobalLayer(1.0, 0.5, N, N, {0.0, 0.0});
-    p.setCostMap(std::vector<std::vector<double>>(N, std::vector<double>(N, 1.0)));
-    if (!p.setGoal(wp(gi, gj))) return 2;
-    const bool r = p.computeTotalCostMap(wp(20, 140));
-    const auto M = p.getTotalCostMatrix();
-    std::vector<double> F((uint64_t)N * N, 1.0), T((uint64_t)N * N);
-    std::vector<uint8_t> closed((uint64_t)N * N);
-    uint64_t pops = 0;
-    const int rr = oracle_fmm_linear(F.data(), N, N, gi, gj, 20, 140, T.data(), closed.data(), &pops);
-    // ties at the exit: the planner replays the reference exactly (exactEarlyExit), so
-    // the whole matrix -- CLOSED values, the band's tentative values, -1 elsewhere --
-    // and every node state are the reference's, bit for bit
-    uint64_t n_closed = 0, bad = 0, band = 0;
-    for (uint64_t k = 0; k < T.size(); ++k) {
-      const double m = M[k / N][k % N];
-      const double want = T[k] < INFINITY ? T[k] : -1.0;
-      if (std::memcmp(&m, &want, sizeof m) != 0) ++bad;
-      const auto node = p.getGlobalNode((unsigned)(k % N), (unsigned)(k / N));
-      if (!node || (node->state == CLOSED) != (closed[k] != 0)) ++bad;
-      n_closed += closed[k] ? 1 : 0;
-      band += (!closed[k] && T[k] < INFINITY) ? 1 : 0;
+    // constant / two-valued cost: mirror images tie, so which cells of exactly the
+    // exit value the reference closed -- and which it reached -- depends on its
+    // insertion order (:551-568).  With the engine's values exact (this double solves
+    // with the oracle's FMM) the planner's order resolution (pop_order.hpp) and band
+    // replay must give the reference's exit state bit for bit, without the exact host
+    // replay: the whole matrix, every node state, the band in insertion order.
+    struct Case {
+      unsigned N, gi, gj, si, sj;
+      bool two;
+    };
+    const Case cases[] = {{160, 80, 80, 20, 140, false}, {96, 48, 48, 48, 20, false},
+                          {97, 30, 30, 60, 60, false},   {64, 2, 5, 40, 40, false},
+                          {120, 60, 60, 100, 30, true},  {90, 45, 20, 45, 70, true}};
+    uint64_t bad = 0;
+    for (const Case& cs : cases) {
+      const unsigned N = cs.N;
+      std::vector<std::vector<double>> cost(N, std::vector<double>(N, 1.0));
+      std::vector<double> F((uint64_t)N * N, 1.0), T((uint64_t)N * N);
+      uint64_t h = 12345;
+      if (cs.two)
+        for (unsigned j = 0; j < N; ++j)
+          for (unsigned i = 0; i < N; ++i) {
+            h = h * 6364136223846793005ull + 1442695040888963407ull;
+            const double v = (h >> 62) ? 1.0 : 2.0;
+            cost[j][i] = v;
+            F[(uint64_t)j * N + i] = v;
+          }
+      DyMuPathPlanner p(1.0, 2.0, 5.0, CONSERVATIVE);
+      p.initGlobalLayer(1.0, 0.5, N, N, {0.0, 0.0});
+      p.setCostMap(cost);
+      if (!p.setGoal(wp(cs.gi, cs.gj))) return 2;
+      const bool r = p.computeTotalCostMap(wp(cs.si, cs.sj));
+      const auto M = p.getTotalCostMatrix();
+      std::vector<uint8_t> closed((uint64_t)N * N);
+      std::vector<uint64_t> seq((uint64_t)N * N);
+      const int rr = oracle_fmm_order(F.data(), N, N, cs.gi, cs.gj, cs.si, cs.sj, T.data(),
+                                      closed.data(), seq.data());
+      uint64_t cbad = 0, band = 0;
+      std::vector<std::pair<uint64_t, uint64_t>> want;  // (seq, k) of the band
+      for (uint64_t k = 0; k < T.size(); ++k) {
+        const double m = M[k / N][k % N];
+        const double w = T[k] < INFINITY ? T[k] : -1.0;
+        if (std::memcmp(&m, &w, sizeof m) != 0) ++cbad;
+        const auto node = p.getGlobalNode((unsigned)(k % N), (unsigned)(k / N));
+        if (!node || (node->state == CLOSED) != (closed[k] != 0)) ++cbad;
+        if (!closed[k] && T[k] < INFINITY) {
+          ++band;
+          want.push_back({seq[k], k});
+        }
+      }
+      std::sort(want.begin(), want.end());
+      const auto nb = p.globalNarrowband();
+      if (p.lastBandSize() != band || nb.size() != band) ++cbad;
+      for (size_t q = 0; q < nb.size() && q < want.size(); ++q) {
+        const uint64_t k = (uint64_t)nb[q].pose.position[1] * N + (uint64_t)nb[q].pose.position[0];
+        if (k != want[q].second) {
+          ++cbad;
+          break;
+        }
+      }
+      const auto& info = p.lastEarlyExitInfo();
+      if (info.exact_replay) ++cbad;
+      std::printf("ties N=%u r=%d oracle=%d band=%llu tied=%llu open=%llu bad=%llu\n", N, (int)r,
+                  rr, (unsigned long long)band, (unsigned long long)info.tied,
+                  (unsigned long long)info.open_at_limit, (unsigned long long)cbad);
+      if ((int)r != rr) ++cbad;
+      bad += cbad;
     }
-    if (p.lastBandSize() != band) ++bad;
-    std::printf("ties r=%d oracle=%d closed=%llu band=%llu bad=%llu\n", (int)r, rr,
-                (unsigned long long)n_closed, (unsigned long long)band, (unsigned long long)bad);
-    return (bad == 0 && (int)r == rr) ? 0 : 1;
+    return bad == 0 ? 0 : 1;
   }
   // >= 1024 rows: getTotalCostMatrix streams the download in row chunks
   const unsigned nx = 300, ny = 1100, gi = 150, gj = 550;

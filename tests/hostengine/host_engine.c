@@ -149,6 +149,20 @@ int dymu_count_equal(dymu_ctx* c, const double* T, uint32_t nx, uint32_t ny, uin
   *count = n;
   return DYMU_OK;
 }
+int dymu_find_equal(dymu_ctx* c, const double* T, uint32_t nx, uint32_t ny, uint64_t ld,
+                    double v, uint64_t* idx, uint64_t cap, uint64_t* count, void* s) {
+  (void)s;
+  if (!c || !count || (cap && !idx)) return DYMU_ERR_ARG;
+  uint64_t n = 0;
+  for (uint32_t j = 0; j < ny; ++j)
+    for (uint32_t i = 0; i < nx; ++i)
+      if (memcmp(&T[(uint64_t)j * ld + i], &v, sizeof v) == 0) {
+        if (n < cap) idx[n] = (uint64_t)j * nx + i;
+        ++n;
+      }
+  *count = n;
+  return DYMU_OK;
+}
 int dymu_scatter(dymu_ctx* c, double* T, uint32_t nx, uint64_t ld, const uint64_t* idx,
                  const double* v, uint64_t n, void* s) {
   (void)s;

@@ -34,6 +34,9 @@ _SIGS = {
                                          ctypes.POINTER(_u64)]),
     "oracle_fmm_heap": (ctypes.c_int, [_dp, _u32, _u32, _u32, _u32, _i64, _i64, _dp, _vp,
                                        ctypes.POINTER(_u64)]),
+    "oracle_fmm_order": (ctypes.c_int, [_dp, _u32, _u32, _u32, _u32, _i64, _i64, _dp, _vp,
+                                        np.ctypeslib.ndpointer(dtype=np.uint64,
+                                                               flags="C_CONTIGUOUS")]),
     "oracle_jacobi": (ctypes.c_int, [_dp, _u32, _u32, _u32, _u32, _dp, ctypes.c_int]),
     "oracle_fim_parallel": (ctypes.c_int, [_dp, _u32, _u32, _u32, _u32, _dp, ctypes.c_int,
                                            ctypes.POINTER(_u64)]),
@@ -252,6 +255,21 @@ class Oracle:
         if want_closed:
             return T, rc, closed
         return T, rc
+
+    def fmm_order(self, F, goal, start=None):
+        """The reference FMM (heap, the linear scan's pop order): T, the return code,
+        the CLOSED mask and each node's band-insertion sequence (uint64 max = never)."""
+        F = np.ascontiguousarray(F, dtype=np.float64)
+        ny, nx = F.shape
+        T = np.empty_like(F)
+        closed = np.zeros((ny, nx), dtype=np.uint8)
+        seq = np.empty((ny, nx), dtype=np.uint64)
+        si, sj = (start if start is not None else (-1, -1))
+        rc = self.lib.oracle_fmm_order(F, nx, ny, goal[0], goal[1], si, sj, T,
+                                       closed.ctypes.data, seq)
+        if rc < 0:
+            raise ValueError("oracle fmm: bad args")
+        return T, rc, closed, seq
 
     def jacobi(self, F, goal, max_sweeps=1 << 30):
         F = np.ascontiguousarray(F, dtype=np.float64)

@@ -45,6 +45,11 @@ int dymu_count_equal(dymu_ctx* c, const double* T, uint32_t nx, uint32_t ny, uin
                      uint64_t* n, void* st) {
   (void)c; (void)T; (void)nx; (void)ny; (void)ld; (void)v; (void)n; (void)st; NODEV;
 }
+int dymu_find_equal(dymu_ctx* c, const double* T, uint32_t nx, uint32_t ny, uint64_t ld, double v,
+                    uint64_t* idx, uint64_t cap, uint64_t* n, void* st) {
+  (void)c; (void)T; (void)nx; (void)ny; (void)ld; (void)v; (void)idx; (void)cap; (void)n; (void)st;
+  NODEV;
+}
 int dymu_scatter(dymu_ctx* c, double* T, uint32_t nx, uint64_t ld, const uint64_t* idx, const double* v,
                  uint64_t n, void* st) {
   (void)c; (void)T; (void)nx; (void)ld; (void)idx; (void)v; (void)n; (void)st; NODEV;

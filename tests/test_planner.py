@@ -255,32 +255,43 @@ def test_config1_exact_call(dymu, oracle, inputs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,g,s", [(160, (80, 80), (20, 140)), (512, (256, 256), (102, 128))])
+@pytest.mark.parametrize("N,g,s", [(160, (80, 80), (20, 140)), (512, (256, 256), (102, 128)),
+                                   (96, (48, 48), (48, 20)), (2048, (1024, 1024), (200, 1900))])
 def test_early_exit_ties_exact(dymu, oracle, N, g, s):
-    """computeTotalCostMap on a constant-speed map, where every axis distance ties
-    with many others: which of the cells of exactly the exit value the reference
-    closed, and so which band cells it reached, depends on its insertion order.  The
-    planner detects the ties (dymu_count_equal, the band replay) and replays the
-    reference exactly on the host: the whole getTotalCostMatrix, every node state,
-    the band (in the reference's insertion order: its first node is the earliest
-    inserted) and the return value are the reference's (linear band, :551-568)."""
+    """computeTotalCostMap on a constant-speed map, where every mirror image ties:
+    which of the cells of exactly the exit value the reference closed, and so which
+    cells it reached, depends on its insertion order (:551-568).  The planner
+    rebuilds that order from the values (csrc/pop_order.hpp) instead of replaying
+    the FMM: the never-reached mask and every node state are the reference's, the
+    values within the parity tolerance, the band in the reference's insertion order
+    (oracle_fmm_order's sequence), and no exact host replay ran."""
     F = np.ones((N, N))
     p = dymu.Planner()
     try:
         p.initGlobalLayer(1.0, 0.5, N, N)
         p.setCostMap(F)
         assert p.setGoal(g)
-        Tl, rc, closed = oracle.fmm(F, g, start=s, linear=True, want_closed=True)
+        Tl, rc, closed, seq = oracle.fmm_order(F, g, start=s)
         assert p.computeTotalCostMap(s) == bool(rc)
+        info = p.lastEarlyExit()
+        assert not info["exact_replay"] and info["tied"] > 1
         M = p.getTotalCostMatrix()
-        want = np.where(np.isfinite(Tl), Tl, -1.0)
-        assert np.array_equal(M.view(np.uint64), want.view(np.uint64))
+        _early_matches(M, Tl)
         band = (closed == 0) & np.isfinite(Tl)
         assert p.lastBandSize() == int(band.sum())
         nb = p.globalNarrowband()
-        assert len(nb) == int(band.sum()) and all(band[j, i] for i, j in nb[:200])
+        bj, bi = np.nonzero(band)
+        want = np.stack([bi, bj], 1)[np.argsort(seq[bj, bi], kind="stable")]
+        assert np.array_equal(nb, want)  # the reference's band vector, in its order
+        if N <= 512:
+            for j in range(N):
+                for i in range(0, N, 7 if N > 160 else 1):
+                    assert p.getGlobalNode(i, j)["state"] == int(closed[j, i]), (i, j)
         for (i, j) in [s, g, (s[0] + 1, s[1]), tuple(nb[0]), tuple(nb[-1])]:
             assert p.getGlobalNode(int(i), int(j))["state"] == int(closed[j, i])
+        (i, j), t = p.minCostGlobalNode()  # first strict minimum in insertion order
+        vals = np.array([M[y, x] for x, y in nb])
+        assert (i, j) == tuple(nb[int(np.argmin(vals))]) and t == vals.min()
     finally:
         p.close()
 
