@@ -805,6 +805,9 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
   }
   early_info_.open_at_limit = open_at_limit_.size();
   bool degenerate = po.degenerate();
+  if (degenerate && std::getenv("DYMU_ORDER_DEBUG"))
+    std::fprintf(stderr, "[dymu] exit order undetermined: reason %d at cell %llu\n", po.why(),
+                 (unsigned long long)po.whyCell());
   if (nb && !degenerate) {
     std::vector<double> vals;
     uint64_t last = s;
@@ -918,6 +921,14 @@ bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& ban
         (int64_t)ny_, {}};
   out.resize(band.size());
   for (size_t q = 0; q < band.size(); ++q) out[q] = rec.val(band[q], last, 0);
+  if (rec.po.degenerate() && std::getenv("DYMU_ORDER_DEBUG")) {
+    const uint64_t k = rec.po.whyCell();
+    std::fprintf(stderr, "[dymu] order undetermined: reason %d at (%llu, %llu) T=%.17g\n",
+                 rec.po.why(), (unsigned long long)(k % nx_), (unsigned long long)(k / nx_), T(k));
+    for (const int64_t d : {-(int64_t)nx_, (int64_t)-1, (int64_t)1, (int64_t)nx_})
+      std::fprintf(stderr, "[dymu]   nb %lld T=%.17g\n", (long long)((int64_t)k + d),
+                   T((uint64_t)((int64_t)k + d)));
+  }
   return rec.po.degenerate();
 }
 

@@ -46,6 +46,8 @@ class PopOrder {
   bool insBefore(uint64_t x, uint64_t y) {
     if (++depth_ > kMaxDepth) {  // nested tie walks: give up rather than recurse on
       degenerate_ = true;
+      why_ = 1;
+      why_cell_ = x;
       --depth_;
       return x < y;
     }
@@ -101,6 +103,8 @@ class PopOrder {
           best = (int64_t)nb[q];
     if (best >= 0 && !(tb < T_(x))) {  // the least neighbour ties with x itself
       degenerate_ = true;
+      why_ = 2;
+      why_cell_ = x;
       best = -1;
     }
     memo_.emplace(x, best);
@@ -108,6 +112,10 @@ class PopOrder {
   }
 
   bool degenerate() const { return degenerate_; }
+  // diagnostics: 1 = tie walks nested too deep, 2 = a node ties with its least
+  // neighbour; the node concerned
+  int why() const { return why_; }
+  uint64_t whyCell() const { return why_cell_; }
 
  private:
   // position of neighbour x in p's nb4List (0 (i,j-1), 1 (i-1,j), 2 (i+1,j), 3 (i,j+1))
@@ -125,6 +133,8 @@ class PopOrder {
   std::unordered_map<uint64_t, int64_t> memo_;
   int depth_ = 0;
   bool degenerate_ = false;
+  int why_ = 0;
+  uint64_t why_cell_ = 0;
 };
 
 template <class TFn>

@@ -82,7 +82,8 @@ int main(int argc, char** argv) {
       unsigned N, gi, gj, si, sj;
       bool two;
     };
-    const Case cases[] = {{160, 80, 80, 20, 140, false}, {96, 48, 48, 48, 20, false},
+    const Case cases[] = {{512, 256, 256, 102, 128, true}, {160, 80, 80, 20, 140, false},
+                          {96, 48, 48, 48, 20, false},
                           {97, 30, 30, 60, 60, false},   {64, 2, 5, 40, 40, false},
                           {120, 60, 60, 100, 30, true},  {90, 45, 20, 45, 70, true}};
     uint64_t bad = 0;

@@ -108,7 +108,8 @@ def _early_matches(M, Tt):
     state: the never-reached mask (-1) exact, CLOSED values and the band's
     tentative values within the parity tolerance."""
     ref = np.where(np.isinf(Tt), -1.0, Tt)
-    assert np.array_equal(M == -1.0, ref == -1.0)
+    bad = np.argwhere((M == -1.0) != (ref == -1.0))
+    assert bad.size == 0, (len(bad), [(tuple(b), M[tuple(b)], ref[tuple(b)]) for b in bad[:8]])
     fin = ref >= 0
     assert (np.abs(M[fin] - ref[fin]) / np.maximum(1, ref[fin])).max() <= RTOL
 
