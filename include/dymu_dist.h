@@ -80,6 +80,11 @@ int dymu_dist_create_peer(dymu_dist** out, dymu_ctx* ctx, int device,
                           const unsigned char id[DYMU_DIST_ID_BYTES], int rank, int world);
 /* DYMU_DIST_RCCL, DYMU_DIST_IPC or DYMU_DIST_PEER */
 int dymu_dist_transport(dymu_dist* d);
+/* Bound on every host wait on a peer rank, process-wide: seconds > 0 overrides
+ * DYMU_DIST_TIMEOUT_S (default 300 s), 0 restores it.  Returns the bound now in
+ * force.  The bench shortens it while it tries candidate transports, so a candidate
+ * that hangs costs seconds, not the run. */
+double dymu_dist_set_timeout(double seconds);
 
 /* Sharded solve of the global grid (nx x ny, goal (goal_i, goal_j) in global
  * coordinates); this rank's slab geometry comes from dymu_slab_rows.

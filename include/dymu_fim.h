@@ -194,6 +194,11 @@ int dymu_dom_exchange(dymu_ctx* ctx, const double* new_lo, const double* new_hi,
  * PREVIOUS round (one launch per round fewer).  Only for domains on kernel 5:
  * DYMU_ERR_STATE otherwise; dymu_dom_round_supported says which (1 / 0). */
 int dymu_dom_round_supported(dymu_ctx* ctx, uint32_t passes);
+/* 1 if a domain of nx x nrows cells would support fused rounds of `passes` (the
+ * check dymu_dom_round_supported makes after dymu_dom_begin), before any domain
+ * exists: the sharded solver's pre-flight rejects an unsupported peer-transport
+ * solve on every rank with DYMU_ERR_ARG instead of aborting the communicator. */
+int dymu_dom_round_capable(dymu_ctx* ctx, uint32_t nx, uint32_t nrows, uint32_t passes);
 int dymu_dom_round(dymu_ctx* ctx, uint32_t passes, const double* new_lo, const double* new_hi,
                    int32_t* d_total, void* stream);
 /* Arm a post for the next launched pass: its block 0 stores *d_src (device

@@ -131,14 +131,18 @@ constexpr const char* kSigMismatch = "the ranks passed different grids, goals or
 
 // Host waits on a peer (an event queued behind RCCL work, a board entry another
 // process writes) are bounded: a peer that died or left the sequence would
-// otherwise block this rank forever.  DYMU_DIST_TIMEOUT_S (default 300 s).
+// otherwise block this rank forever.  DYMU_DIST_TIMEOUT_S (default 300 s), or the
+// process-wide override of dymu_dist_set_timeout (the bench's candidate tuning).
+std::atomic<double> g_timeout_override{0.0};
+
 double dist_timeout_s() {
   static const double limit_s = [] {
     const char* kv = std::getenv("DYMU_DIST_TIMEOUT_S");
     const double v = kv ? std::atof(kv) : 0.0;
     return v > 0.0 ? v : 300.0;
   }();
-  return limit_s;
+  const double o = g_timeout_override.load(std::memory_order_relaxed);
+  return o > 0.0 ? o : limit_s;
 }
 
 // spin on cond() with a pause, then short sleeps; false after the timeout
@@ -1055,6 +1059,12 @@ const char* dymu_dist_last_error(dymu_dist* d) { return d ? d->last_error.c_str(
 
 int dymu_dist_transport(dymu_dist* d) { return d ? d->kind : DYMU_ERR_ARG; }
 
+double dymu_dist_set_timeout(double seconds) {
+  const double prev = g_timeout_override.exchange(seconds > 0.0 ? seconds : 0.0);
+  (void)prev;
+  return dist_timeout_s();
+}
+
 int dymu_dist_comm_count(dymu_dist* d, int* ranks) {
   if (!d || !ranks) return DYMU_ERR_ARG;
   if (!d->xp || d->aborted) return DYMU_ERR_STATE;
@@ -1079,9 +1089,19 @@ int dymu_dist_solve(dymu_dist* d, const double* F_slab, double* T_buf, uint64_t 
   std::vector<Local> L(1);
   L[0].ctx = d->ctx;
   L[0].rank = d->rank;
-  const bool ok = nx > 0 && ny > 0 && goal_i < nx && goal_j < ny &&
-                  make_slab(F_slab, T_buf, ld, nx, ny, goal_j, d->rank, d->world, &L[0].s) == DYMU_OK;
+  bool ok = nx > 0 && ny > 0 && goal_i < nx && goal_j < ny &&
+            make_slab(F_slab, T_buf, ld, nx, ny, goal_j, d->rank, d->world, &L[0].s) == DYMU_OK;
+  // the peer transport runs fused kernel-5 rounds (K >= 2, not deterministic): an
+  // unsupported solve is an argument error on every rank, before any collective
+  // state changes, so the communicator stays usable
+  const bool peer_ok = d->kind != DYMU_DIST_PEER || !ok ||
+                       dymu_dom_round_capable(d->ctx, nx, L[0].s.dom.nrows, K) == 1;
+  ok = ok && peer_ok;
   int rc = d->xp->preflight(ok, call_signature(nx, ny, goal_i, goal_j, K), st, err);
+  if (rc == DYMU_ERR_ARG && !peer_ok)
+    return fail(err, "dymu_dist_solve",
+                "the peer transport needs kernel-5 slabs, K >= 2 and a non-deterministic engine",
+                DYMU_ERR_ARG);
   if (rc) return rc == DYMU_ERR_ARG ? rc : abort_dist(d, rc);
   // receive rows only after every rank accepted this solve (its signature pins nx): a
   // rank whose arguments were rejected must not re-allocate (and re-publish) alone, or

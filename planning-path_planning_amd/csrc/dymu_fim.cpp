@@ -237,10 +237,8 @@ void dom_retire(dymu_ctx* c) {
 // need_keys: the caller needs tile keys (lower bounds on every value the passes can
 // still produce, dymu_solve_until_device): the plain FIM kernel 3 has none, kernel 4
 // runs instead.
-int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t nrows, uint64_t ld,
-              int ghost_lo, int ghost_hi, int64_t gi, int64_t gj, hipStream_t st,
-              bool cold = true, bool need_keys = false) {
-  if (!dF || !dT || nx == 0 || nrows == 0 || ld < nx) return DYMU_ERR_ARG;
+// the pass kernel a domain of nx x nrows cells runs
+int dom_variant(const dymu_ctx* c, uint32_t nx, uint32_t nrows, bool need_keys) {
   int variant = c->variant;
   if (variant == 0) {
     const uint64_t t8 = (uint64_t)((nx + kWaveTile - 1) / kWaveTile) *
@@ -249,6 +247,14 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   }
   if (need_keys && !is_prio(variant)) variant = 4;
   if (c->opts.deterministic) variant = 5;
+  return variant;
+}
+
+int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t nrows, uint64_t ld,
+              int ghost_lo, int ghost_hi, int64_t gi, int64_t gj, hipStream_t st,
+              bool cold = true, bool need_keys = false) {
+  if (!dF || !dT || nx == 0 || nrows == 0 || ld < nx) return DYMU_ERR_ARG;
+  const int variant = dom_variant(c, nx, nrows, need_keys);
   const int TWd = tile_w(variant), THd = tile_h(variant);
   if (ghost_hi && (nrows % (uint32_t)THd) != 0) return DYMU_ERR_ARG;
   if (gj >= 0 && (gi < 0 || gi >= (int64_t)nx || gj >= (int64_t)nrows)) return DYMU_ERR_ARG;
@@ -1478,6 +1484,11 @@ int dymu_dom_exchange(dymu_ctx* c, const double* new_lo, const double* new_hi,
 
 int dymu_dom_round_supported(dymu_ctx* c, uint32_t passes) {
   return c && dom_round_ok(c, passes) ? 1 : 0;
+}
+
+int dymu_dom_round_capable(dymu_ctx* c, uint32_t nx, uint32_t nrows, uint32_t passes) {
+  if (!c || nx == 0 || nrows == 0) return 0;
+  return dom_variant(c, nx, nrows, false) == 5 && passes >= 2 && !c->opts.deterministic ? 1 : 0;
 }
 
 int dymu_dom_round(dymu_ctx* c, uint32_t passes, const double* new_lo, const double* new_hi,

@@ -1440,13 +1440,16 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
         const double* src = side == 0 ? a.merge_lo : a.merge_hi;
         if (!src) continue;
         const bool tagged = a.merge_tag[side] != nullptr;  // peer rounds: a neighbour writes src
-        if (tagged && m0 < m1 && lane == 0) {
+        if (tagged && m0 < m1) {
           // the tag first: the rows of every push up to it are complete (the pusher's
-          // release); R = the smallest tag any workgroup read (status pass)
+          // release); R = the smallest tag any workgroup read (status pass).  Every lane
+          // performs the acquire, so each lane's row loads below are ordered after it by
+          // the memory model, not only by the wave's lockstep (one line)
           const unsigned long long t = __hip_atomic_load(a.merge_tag[side], __ATOMIC_ACQUIRE,
                                                          __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_fetch_min(&a.peer->rmin[side], t, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0)
+            __hip_atomic_fetch_min(&a.peer->rmin[side], t, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
         double* gh = a.T + (side == 0 ? -a.ld : a.ny * a.ld);
         const uint32_t trow = side == 0 ? 0u : (uint32_t)(a.nty - 1);

@@ -123,6 +123,7 @@ FIM_SYMBOLS = {
     "dymu_dom_pending": (_i32, [_vp, _vp, ctypes.POINTER(_u64)]),
     "dymu_dom_exchange": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dymu_dom_round_supported": (_i32, [_vp, _u32]),
+    "dymu_dom_round_capable": (_i32, [_vp, _u32, _u32, _u32]),
     "dymu_dom_round": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp]),
     "dymu_dom_round_peer": (_i32, [_vp, _u32, _vp, _vp]),
     "dymu_count_equal": (_i32, [_vp, _vp, _u32, _u32, _u64, ctypes.c_double,

@@ -42,6 +42,7 @@ DIST_SYMBOLS = {
     "dymu_dist_create_ipc": (_i32, [ctypes.POINTER(_vp), _vp, _i32, ctypes.c_char_p, _i32, _i32]),
     "dymu_dist_create_peer": (_i32, [ctypes.POINTER(_vp), _vp, _i32, ctypes.c_char_p, _i32, _i32]),
     "dymu_dist_transport": (_i32, [_vp]),
+    "dymu_dist_set_timeout": (ctypes.c_double, [ctypes.c_double]),
     "dymu_dist_last_error": (ctypes.c_char_p, [_vp]),
     "dymu_dist_comm_count": (_i32, [_vp, ctypes.POINTER(ctypes.c_int)]),
 }
@@ -66,6 +67,12 @@ def load_dist() -> ctypes.CDLL:
 
 
 TRANSPORTS = ("rccl", "ipc", "peer")
+
+
+def set_timeout(seconds: float) -> float:
+    """Process-wide bound on every host wait on a peer rank (0: DYMU_DIST_TIMEOUT_S /
+    300 s again); returns the bound in force."""
+    return float(load_dist().dymu_dist_set_timeout(float(seconds)))
 
 
 def unique_id(transport: str = "rccl") -> bytes:

@@ -101,6 +101,24 @@ def test_bench_gpus2_one_gpu_transport_choice_self_check():
 
 
 @pytest.mark.gpu
+def test_bench_gpus2_candidate_failure_dropped_with_reason():
+    """A candidate transport that fails while the bench times the candidates (here
+    forced on rank 1 by DYMU_BENCH_FAIL_CANDIDATE) is dropped on every rank with its
+    reason, under the tuning's short wait bound, and the line still prints with the
+    other transport and a passing self-check (VERDICT r4 "do this" 4)."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--size", "1024", "--steps", "1", "--warmup", "1", "--cpu-sample", "0"],
+                         env=_env(DYMU_DIST_TIMEOUT_S="60", DYMU_BENCH_FAIL_CANDIDATE="peer:1"),
+                         cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    cfg = rec["config"]
+    assert cfg["transport"] == "ipc" and rec["parity"]["ok"]
+    assert "peer" in cfg["transports_dropped"] and "timing" in cfg["transports_dropped"]["peer"]
+    assert sorted(cfg["k_autotune_ms"]) == ["ipc"]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("exchange", ["ipc", "peer"])
 def test_bench_gpus2_fixed_transport_self_check(exchange):
     """`--exchange ipc|peer` runs that transport only, with its self-check."""

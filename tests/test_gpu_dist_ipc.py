@@ -39,9 +39,10 @@ def _worker(rank, world, uid, nx, ny, goal, F_full, out_q, engine_kw, bad_rank, 
         if bad_rank is not None:  # one rank passes an invalid slab / another K: all refuse
             bad = rank == bad_rank
             wide = nx + 64 if bad and bad_kind == "nx" else nx  # a wider grid (and pitch)
+            K = 1 if bad_kind == "k1" else (3 if bad and bad_kind == "k" else 4)
             try:
                 solver.solve(0 if bad and bad_kind == "slab" else dF, dT, wide, wide, ny, goal[0],
-                             goal[1], 3 if bad and bad_kind == "k" else 4)
+                             goal[1], K)
                 pre = "solved"
             except dymu.DymuError as e:
                 pre = e.status
@@ -131,10 +132,12 @@ def test_peer_loop_across_processes_matches_oracle(dymu, oracle, world, nx, ny, 
     _run(oracle, world, nx, ny, goal, engine_kw, transport="peer", obst=obst)
 
 
-@pytest.mark.parametrize("bad_kind", ["slab", "nx"])
+@pytest.mark.parametrize("bad_kind", ["slab", "nx", "k1"])
 def test_peer_preflight_rejects_on_every_rank(dymu, oracle, bad_kind):
     """The peer transport's pre-flight (the same board as IPC): a rank-local error
     fails every rank with DYMU_ERR_ARG; the following solves reset the receive rows
-    and match the oracle."""
+    and match the oracle.  "k1": every rank asks for K = 1, which the peer transport's
+    fused rounds cannot run -- rejected before any collective state changes, so the
+    communicator survives (it used to abort every later solve)."""
     _run(oracle, 3, 160, 200, (80, 100), dict(kernel=5, prio_target=8), bad_rank=1,
          bad_kind=bad_kind, transport="peer")
