@@ -87,6 +87,8 @@ struct dymu_ctx {
   unsigned long long* h_probe = nullptr;  // pinned [2]: early-exit probe (max T, min key)
   uint64_t* d_band = nullptr;   // early-exit band indices (device)
   uint64_t band_cap = 0;
+  void* d_xfer = nullptr;       // staging of dymu_find_equal / dymu_scatter (device)
+  uint64_t xfer_cap = 0;        // bytes
   unsigned long long* d_scratch = nullptr;  // 8 words of per-call device scalars
   double* d_lut = nullptr;      // computeCostMap LUT (device copy)
   size_t lut_cap = 0;
@@ -188,6 +190,17 @@ int ensure_prio(dymu_ctx* c, uint32_t ntiles) {
   c->keys_cap = 0;
   HIPC(c, hipMalloc(&c->d_keys, sizeof(unsigned long long) * 3ull * ntiles));
   c->keys_cap = ntiles;
+  return DYMU_OK;
+}
+
+int ensure_xfer(dymu_ctx* c, uint64_t bytes) {
+  if (bytes <= c->xfer_cap) return DYMU_OK;
+  if (c->d_xfer) HIPC(c, hipFree(c->d_xfer));
+  c->d_xfer = nullptr;
+  c->xfer_cap = 0;
+  bytes = std::max<uint64_t>(bytes, 1u << 16);
+  HIPC(c, hipMalloc(&c->d_xfer, bytes));
+  c->xfer_cap = bytes;
   return DYMU_OK;
 }
 
@@ -1220,6 +1233,7 @@ int dymu_destroy(dymu_ctx* c) {
   if (c->h_probe) (void)hipHostFree(c->h_probe);
   if (c->h_mail) (void)hipHostFree(c->h_mail);
   if (c->d_band) (void)hipFree(c->d_band);
+  if (c->d_xfer) (void)hipFree(c->d_xfer);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return DYMU_OK;
@@ -1306,21 +1320,17 @@ int dymu_find_equal(dymu_ctx* c, const double* dT, uint32_t nx, uint32_t ny, uin
   if (!c || !dT || !count || ld < nx || (cap && !idx)) return DYMU_ERR_ARG;
   HIPC(c, hipSetDevice(c->device));
   hipStream_t st = pick_stream(c, stream);
+  int rc = ensure_xfer(c, sizeof(uint64_t) * (cap ? cap : 1));
+  if (rc) return rc;
+  uint64_t* di = static_cast<uint64_t*>(c->d_xfer);
   unsigned long long* cnt = c->d_scratch + 4;
-  uint64_t* di = nullptr;
-  const uint64_t dcap = cap ? cap : 1;
-  HIPC(c, hipMallocAsync(reinterpret_cast<void**>(&di), sizeof(uint64_t) * dcap, st));
-  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st);
-  if (e == hipSuccess) e = launch_count_equal(dT, (int64_t)ld, nx, ny, value, cnt, di, cap, st);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(c->h_probe, cnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  const uint64_t m = e == hipSuccess ? std::min<uint64_t>(c->h_probe[0], cap) : 0;
-  if (m) e = hipMemcpy(idx, di, sizeof(uint64_t) * m, hipMemcpyDeviceToHost);
-  (void)hipFreeAsync(di, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess) return fail_hip(c, e, "dymu_find_equal");
+  HIPC(c, hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
+  HIPC(c, launch_count_equal(dT, (int64_t)ld, nx, ny, value, cnt, di, cap, st));
+  HIPC(c, hipMemcpyAsync(c->h_probe, cnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  HIPC(c, hipStreamSynchronize(st));
   *count = c->h_probe[0];
+  const uint64_t m = std::min<uint64_t>(*count, cap);
+  if (m) HIPC(c, hipMemcpy(idx, di, sizeof(uint64_t) * m, hipMemcpyDeviceToHost));
   return DYMU_OK;
 }
 
@@ -1330,17 +1340,19 @@ int dymu_scatter(dymu_ctx* c, double* dT, uint32_t nx, uint64_t ld, const uint64
   if (n == 0) return DYMU_OK;
   HIPC(c, hipSetDevice(c->device));
   hipStream_t st = pick_stream(c, stream);
-  uint64_t* di = nullptr;
-  double* dv = nullptr;
-  HIPC(c, hipMallocAsync(reinterpret_cast<void**>(&di), sizeof(uint64_t) * n, st));
-  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&dv), sizeof(double) * n, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(di, idx, sizeof(uint64_t) * n, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(dv, vals, sizeof(double) * n, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = launch_scatter(dT, (int64_t)ld, nx, di, dv, n, st);
-  if (dv) (void)hipFreeAsync(dv, st);
-  (void)hipFreeAsync(di, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess) return fail_hip(c, e, "dymu_scatter");
+  // a context-owned staging buffer and blocking copies: the stream-ordered pool
+  // allocation with asynchronous pageable copies this replaced delivered zeros to the
+  // kernel after an earlier free in the same stream (round 5: the early exit wrote
+  // T = 0 into cell 0)
+  int rc = ensure_xfer(c, (sizeof(uint64_t) + sizeof(double)) * n);
+  if (rc) return rc;
+  uint64_t* di = static_cast<uint64_t*>(c->d_xfer);
+  double* dv = reinterpret_cast<double*>(di + n);
+  HIPC(c, hipStreamSynchronize(st));
+  HIPC(c, hipMemcpy(di, idx, sizeof(uint64_t) * n, hipMemcpyHostToDevice));
+  HIPC(c, hipMemcpy(dv, vals, sizeof(double) * n, hipMemcpyHostToDevice));
+  HIPC(c, launch_scatter(dT, (int64_t)ld, nx, di, dv, n, st));
+  HIPC(c, hipStreamSynchronize(st));
   return DYMU_OK;
 }
 

@@ -15,7 +15,7 @@
 #   vdist=N[:K[:S...]]    tools/vdist_rehearsal.py N K S... (1-8 virtual ranks)
 #   prof=VTAG             tools/prof_r03.sh (rocprofv3 --stats + PMC passes)
 #   py=SCRIPT[:ARGS]      python SCRIPT ARGS (any other tool), output SCRIPT.out
-# Other steps take ':'-separated arguments (tests=tests/test_planner.py:-k:ties).
+# Other steps take ':'-separated arguments (tests=tests/test_planner.py:-k:ties~or~exit).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 TAG=$1; shift
@@ -34,7 +34,9 @@ for step in "$@"; do
   key=${step%%=*}; val=; [ "$key" != "$step" ] && val=${step#*=}
   [ "$key" != py ] && val=${val//:/ }  # ':' separates arguments (vdist=16384:4)
   case $key in
-    tests) run tests 1100 python -u -m pytest ${val:-tests} -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    tests) # '~' inside an argument stands for a space (tests=tests/x.py:-k:a~or~b)
+           args=(); for w in ${val:-tests}; do args+=("${w//\~/ }"); done
+           run tests 1100 python -u -m pytest "${args[@]}" -m gpu -x -v --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py $val ;;
     quick) run quick 300 python -u bench.py --no-planner --cpu-sample 0 --no-variants --steps 10 --warmup 2 ;;
