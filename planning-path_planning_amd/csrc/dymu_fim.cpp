@@ -74,7 +74,6 @@ struct dymu_ctx {
   uint32_t* d_lists = nullptr;       // 3 lists x kShards shards x tiles_cap
   uint32_t* d_counts = nullptr;      // 3 x kShards words, own block
   uint32_t* d_tile_epoch = nullptr;  // tiles_cap
-  uint32_t* d_vstamp = nullptr;      // tiles_cap: per-pass visit claims (chained visits)
   unsigned long long* d_stats = nullptr;  // kStatSlots
   // v4 priority state: keys 3 x tiles_cap, hist 3 x kShards x kBins,
   // prio = {minkey[3] (u64), base[3] (f64), delta (f64)}
@@ -165,16 +164,12 @@ int ensure_tiles(dymu_ctx* c, uint32_t ntiles, hipStream_t st) {
   if (ntiles <= c->tiles_cap) return DYMU_OK;
   if (c->d_lists) (void)hipFree(c->d_lists);
   if (c->d_tile_epoch) (void)hipFree(c->d_tile_epoch);
-  if (c->d_vstamp) (void)hipFree(c->d_vstamp);
   c->d_lists = nullptr;
   c->d_tile_epoch = nullptr;
-  c->d_vstamp = nullptr;
   c->tiles_cap = 0;
   HIPC(c, hipMalloc(&c->d_lists, sizeof(uint32_t) * 3ull * kShards * ntiles));
   HIPC(c, hipMalloc(&c->d_tile_epoch, sizeof(uint32_t) * (uint64_t)ntiles));
   HIPC(c, hipMemsetAsync(c->d_tile_epoch, 0, sizeof(uint32_t) * (uint64_t)ntiles, st));
-  HIPC(c, hipMalloc(&c->d_vstamp, sizeof(uint32_t) * (uint64_t)ntiles));
-  HIPC(c, hipMemsetAsync(c->d_vstamp, 0, sizeof(uint32_t) * (uint64_t)ntiles, st));
   c->tiles_cap = ntiles;
   c->epoch_base = 0;
   return DYMU_OK;
@@ -291,7 +286,6 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
   D.max_passes = c->opts.max_passes > 0 ? (uint64_t)c->opts.max_passes : 4ull * ntiles + 1024ull;
   if ((uint64_t)c->epoch_base + D.max_passes + kPassSlack + 8 >= 0xFFFFFFF0ull) {
     HIPC(c, hipMemsetAsync(c->d_tile_epoch, 0, sizeof(uint32_t) * (uint64_t)ntiles, st));
-    HIPC(c, hipMemsetAsync(c->d_vstamp, 0, sizeof(uint32_t) * (uint64_t)ntiles, st));
     c->epoch_base = 0;
   }
   D.eb = c->epoch_base;
@@ -406,15 +400,6 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
     HIPC(c, hipMemsetAsync(c->d_hist + (uint64_t)3 * kShards * kBins, 0,
                            sizeof(uint32_t) * 2 * kShards * kBins, st));
   }
-  // chained visits in short-list passes: kernel 5, not deterministic
-  a.vstamp = c->d_vstamp;
-  a.chain_below = 0u;
-  a.chain_hops = 4u;
-  a.chain_ticks = 2500u;
-  if (const char* kv = std::getenv("DYMU_CHAIN_BELOW")) a.chain_below = (uint32_t)std::max(0, std::atoi(kv));
-  if (const char* kv = std::getenv("DYMU_CHAIN_HOPS")) a.chain_hops = (uint32_t)std::max(1, std::atoi(kv));
-  if (const char* kv = std::getenv("DYMU_CHAIN_TICKS")) a.chain_ticks = (uint32_t)std::max(0, std::atoi(kv));
-  if (variant != 5 || c->opts.deterministic) a.chain_below = 0u;
   a.shard_cap = ntiles;
   a.tile_epoch = c->d_tile_epoch;
   a.stats = c->d_stats;
@@ -1215,7 +1200,6 @@ int dymu_destroy(dymu_ctx* c) {
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->d_lists) (void)hipFree(c->d_lists);
   if (c->d_tile_epoch) (void)hipFree(c->d_tile_epoch);
-  if (c->d_vstamp) (void)hipFree(c->d_vstamp);
   if (c->d_counts) (void)hipFree(c->d_counts);
   if (c->d_keys) (void)hipFree(c->d_keys);
   if (c->d_hist) (void)hipFree(c->d_hist);

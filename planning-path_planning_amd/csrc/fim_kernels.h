@@ -127,16 +127,6 @@ struct PassArgs {
   // load, one at or below it is relaxed without waiting on the key (the current key
   // is never above the first-insertion one, so the decision is the key gate's)
   int pack_bins;
-  // ---- kernel 5: chained visits in short-list passes ----
-  // a pass whose list holds at most chain_below tiles lets a wave go on from the
-  // tile it relaxed into the activated neighbour of least key, up to chain_hops
-  // visits in all and while the pass is younger than chain_ticks (10-ns ticks),
-  // instead of queueing that neighbour for the next pass.  Every visit of such a
-  // pass first claims its tile (atomicMax(vstamp[t], epoch)): a tile is relaxed at
-  // most once per pass, so no visit can load a tile another CU wrote this pass.
-  // chain_below = 0: off.
-  uint32_t* vstamp;
-  uint32_t chain_below, chain_hops, chain_ticks;
 };
 // list entries: the tile index in the low kPackShift bits; bits above: 0 = no bin
 // (seeding kernels, merges), else the key bin + 1 the entry was first inserted with

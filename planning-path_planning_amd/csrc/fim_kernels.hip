@@ -96,14 +96,6 @@ __device__ __forceinline__ uint32_t list_at(const uint32_t* list, uint32_t cap,
   return list[(uint64_t)k * cap + (li - pref[k])];
 }
 
-// the 64-bit value of lane l (wave-uniform l), in scalar registers
-__device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-  return ((unsigned long long)hi << 32) | lo;
-}
-constexpr uint32_t kNoTile = 0xFFFFFFFFu;
-
 // list_at for a wave-uniform li: lane q reads pref[q], one ballot counts the
 // shards that start at or before li (one LDS read and a few VALU ops instead of
 // fifteen reads and a 64-bit add chain)
@@ -1248,7 +1240,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   unsigned long long* trace = a.trace ? a.trace + (uint64_t)blockIdx.x * kTracePts : nullptr;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   // no deadline: 2^30 ticks (10.7 s) ahead, far beyond any pass
-  uint32_t stop_at = (uint32_t)t_start + (a.sweep_deadline ? a.sweep_deadline : (1u << 30));
+  const uint32_t stop_at = (uint32_t)t_start + (a.sweep_deadline ? a.sweep_deadline : (1u << 30));
   if (trace && tid == 0) trace[0] = t_start;
 
   const double delta = *a.delta;
@@ -1296,11 +1288,6 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   __syncthreads();
   const uint32_t n_active = s_pref[kShards];
   const int bstar = s_bstar;
-  // a short list: chained visits (PassArgs::vstamp), with the sweep deadline moved
-  // past the chaining window so that a chained visit still converges its tile
-  const bool chain = a.chain_below != 0u && n_active <= a.chain_below;
-  const uint32_t chain_stop = (uint32_t)t_start + a.chain_ticks;
-  if (chain && a.sweep_deadline) stop_at = chain_stop + a.sweep_deadline;
   if (trace && tid == 0) trace[1] = __builtin_amdgcn_s_memrealtime();
   if (blockIdx.x == 0) {
     if (tid < kShards) a.count_clear[tid] = 0u;
@@ -1352,80 +1339,50 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   const uint32_t nb = gridDim.x;
   bool first = true;
   if (trace && tid == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
-  uint32_t ctile = kNoTile;  // chained visit: the tile to relax next, and its key
-  unsigned long long ckey = 0;
-  uint32_t hops = 0;
   for (;;) {  // wave-uniform
-    const bool chained = ctile != kNoTile;
-    uint32_t tile;
-    unsigned long long kb;
-    bool decided;
-    if (chained) {  // the neighbour the previous visit activated: no list entry, no gate
-      tile = ctile;
-      kb = ckey;
-      decided = true;
-      ctile = kNoTile;
-      ++hops;
-    } else {
-      hops = 0;
-      uint32_t e = 0;
-      if (lane == 0) e = blockIdx.x + atomicAdd(&s_next, 1u) * nb;
-      e = __builtin_amdgcn_readfirstlane(e);
-      if (e >= n_active) break;
-      const uint32_t ent =
-          __builtin_amdgcn_readfirstlane(list_at_wave(a.list_in, a.shard_cap, s_pref, e, lane));
-      tile = ent & kTileMask;
-      const int pbin = (int)(ent >> kPackShift) - 1;  // first-insertion bin, -1: none
-      const int tx0 = (int)(tile % (uint32_t)a.ntx);
-      const int ty0 = (int)(tile / (uint32_t)a.ntx);
-      if (a.checker && ((uint32_t)(tx0 + ty0) + a.checker_parity) % 2u != 0u) {
-        // the other colour of the checkerboard: deferred with its key, tile not loaded
-        if (lane == 0) {
-          const unsigned long long k0 = a.key_in[tile];
-          a.key_in[tile] = kInfBits;
-          enqueue(tile, k0);
-        }
-        ++my_defer;
-        if (STATS && a.pstat) ++my_cd;
-        continue;
-      }
-      kb = a.key_in[tile];
-      // a packed bin at or below b*: admitted (the current key is no higher); above: the
-      // current key decides now, before the tile loads a deferral would waste
-      if (pbin > bstar && key_bin(bitsd(kb), origin_in, inv_delta) > bstar) {
-        if (lane == 0) {
-          a.key_in[tile] = kInfBits;
-          enqueue(tile, kb);
-        }
-        ++my_defer;
-        continue;
-      }
-      decided = pbin >= 0;
-    }
+    uint32_t e = 0;
+    if (lane == 0) e = blockIdx.x + atomicAdd(&s_next, 1u) * nb;
+    e = __builtin_amdgcn_readfirstlane(e);
+    if (e >= n_active) break;
+    const uint32_t ent =
+        __builtin_amdgcn_readfirstlane(list_at_wave(a.list_in, a.shard_cap, s_pref, e, lane));
+    const uint32_t tile = ent & kTileMask;
+    const int pbin = (int)(ent >> kPackShift) - 1;  // first-insertion bin, -1: none
     const int tx = (int)(tile % (uint32_t)a.ntx);
     const int ty = (int)(tile / (uint32_t)a.ntx);
-    // chain passes: claim the tile for this pass before relaxing it (the atomic's
-    // latency overlaps the tile loads; the gate waits on it)
-    uint32_t claim = 0u;
-    if (chain && lane == 0) claim = atomicMax(&a.vstamp[tile], a.epoch);
-    bool claimed = true;
+    if (a.checker && ((uint32_t)(tx + ty) + a.checker_parity) % 2u != 0u) {
+      // the other colour of the checkerboard: deferred with its key, tile not loaded
+      if (lane == 0) {
+        const unsigned long long k0 = a.key_in[tile];
+        a.key_in[tile] = kInfBits;
+        enqueue(tile, k0);
+      }
+      ++my_defer;
+      if (STATS && a.pstat) ++my_cd;
+      continue;
+    }
+    const unsigned long long kb = a.key_in[tile];
+    // a packed bin at or below b*: admitted (the current key is no higher); above: the
+    // current key decides now, before the tile loads a deferral would waste
+    if (pbin > bstar && key_bin(bitsd(kb), origin_in, inv_delta) > bstar) {
+      if (lane == 0) {
+        a.key_in[tile] = kInfBits;
+        enqueue(tile, kb);
+      }
+      ++my_defer;
+      continue;
+    }
+    const bool decided = pbin >= 0;
     if (lane < 4) ek[lane] = kInfBits;
     if (trace && tid == 0 && first) trace[6] = __builtin_amdgcn_s_memrealtime();
     bool capped = false;
     const int sweeps = visit16<APPROX>(
         a, img, ek, true, tx, ty, lane, capped,
-        [&] {
-          if (chain) claimed = __builtin_amdgcn_readfirstlane(claim) < a.epoch;
-          return claimed && (decided || key_bin(bitsd(kb), origin_in, inv_delta) <= bstar);
-        },
-        stop_at);
-    if (lane == 0 && !chained) a.key_in[tile] = kInfBits;
-    if (sweeps < 0) {
-      // key-deferred: to the next pass with its key.  A listed tile another wave's
-      // chain already relaxed this pass is done; a chain target claimed elsewhere is
-      // queued like any activation
-      if (lane == 0 && (claimed || chained)) enqueue(tile, kb);
-      if (claimed) ++my_defer;
+        [&] { return decided || key_bin(bitsd(kb), origin_in, inv_delta) <= bstar; }, stop_at);
+    if (lane == 0) a.key_in[tile] = kInfBits;
+    if (sweeps < 0) {  // deferred to the next pass with its key
+      if (lane == 0) enqueue(tile, kb);
+      ++my_defer;
       continue;
     }
     if (trace && tid == 0 && first) {
@@ -1460,34 +1417,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       want = true;
       k2 = kb;
     }
-    // chain: go on into the activated neighbour of least key now, instead of queueing it
-    int sel = -1;
-    if (chain && hops + 1u < a.chain_hops &&
-        (int32_t)(chain_stop - (uint32_t)__builtin_amdgcn_s_memrealtime()) > 0) {
-      const unsigned long long kc = (lane < 4 && want) ? k2 : ~0ull;
-      unsigned long long best = ~0ull;
-#pragma unroll
-      for (int l = 0; l < 4; ++l) {
-        const unsigned long long v = readlane64(kc, l);
-        if (v < best) {
-          best = v;
-          sel = l;
-        }
-      }
-      if (sel >= 0) {
-        const int cx = sel == 1 ? tx - 1 : sel == 2 ? tx + 1 : tx;
-        const int cy = sel == 0 ? ty - 1 : sel == 3 ? ty + 1 : ty;
-        ctile = (uint32_t)cy * (uint32_t)a.ntx + (uint32_t)cx;
-        ckey = best;
-      }
-    }
-    if (want && lane != sel) enqueue((uint32_t)ny_t * (uint32_t)a.ntx + (uint32_t)nx_t, k2);
-    if (sel >= 0) {
-      // the next visit loads what this one wrote (its edge rows / columns, other lanes):
-      // the stores complete before those loads (one workgroup, one L1)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    }
+    if (want) enqueue((uint32_t)ny_t * (uint32_t)a.ntx + (uint32_t)nx_t, k2);
     __builtin_amdgcn_wave_barrier();
     if (trace && first) {
       __builtin_amdgcn_s_waitcnt(0);
