@@ -47,7 +47,7 @@ for step in "$@"; do
     vdist) run "vdist${val// /_}" 600 python -u tools/vdist_rehearsal.py $val ;;
     prof) VTAG=$val run prof 900 bash tools/prof_r03.sh ;;
     py) s=${val%%:*}; a=; [ "$s" != "$val" ] && a=${val#*:}
-        run "$(basename "$s" .py)" 600 python -u "$s" $a ;;
+        run "$(basename "$s" .py)" 600 python -u "$s" ${a//:/ } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
