@@ -727,14 +727,6 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
   }
   band.resize(nb);
   std::sort(band.begin(), band.end());
-  const bool dbg = std::getenv("DYMU_ORDER_DEBUG") != nullptr;
-  auto probe0 = [&](const char* where) {
-    if (!dbg) return;
-    double d0 = -2.0;
-    (void)dymu_memcpy_d2h(ctx_, &d0, dT_, sizeof d0);
-    std::fprintf(stderr, "[dymu]   dT[0] %s: %g\n", where, d0);
-  };
-  probe0("after mask");
   const auto t0 = std::chrono::steady_clock::now();
   const uint64_t g = idx(goal_i_, goal_j_), s = idx(si, sj);
   auto mirror = [this](uint64_t k) { return T(k); };
@@ -753,7 +745,6 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
       eq.resize(n_eq);
     }
     eq.resize(n_eq);
-    probe0("after find_equal");
     early_info_.tied = n_eq;
     if (n_eq > 1) {
       const uint64_t probes[5] = {s, s - nx_, s - 1, s + 1, s + nx_};
@@ -823,17 +814,10 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
     for (const uint64_t q : {s - nx_, s - 1, s + 1, s + nx_})
       if (closedCell(q) && po.popBefore(last, q)) last = q;
     degenerate = replayBand(last, band, vals);
-    probe0("after replay");
-    if (dbg)
-      for (uint64_t q = 0; q < nb; ++q)
-        if (band[q] == 0 || vals[q] == 0.0)
-          std::fprintf(stderr, "[dymu]   band[%llu] = %llu val %g\n", (unsigned long long)q,
-                       (unsigned long long)band[q], vals[q]);
     if (!degenerate) {
       rc = dymu_scatter(ctx_, dT_, nx_, nx_, band.data(), vals.data(), nb, nullptr);
       if (rc != DYMU_OK)
         throw std::runtime_error(std::string("dymu_scatter failed: ") + dymu_last_error(ctx_));
-      probe0("after scatter");
       // blocks fetched during the replay hold the pre-replay band values
       for (uint64_t q = 0; q < nb; ++q) total_cost_[band[q]] = vals[q];
     }
@@ -853,16 +837,11 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
              "them is not reproduced (grid larger than the exact-replay limit)");
     open_at_limit_.clear();
   }
-  if (std::getenv("DYMU_ORDER_DEBUG")) {
-    double d0 = -2.0;
-    (void)dymu_memcpy_d2h(ctx_, &d0, dT_, sizeof d0);
-    std::fprintf(stderr,
-                 "[dymu] early exit: t_closed %.17g band %llu tied %llu open %llu degenerate %d "
-                 "T(0) host %g device %g blk0 %d\n",
-                 t_closed, (unsigned long long)nb, (unsigned long long)early_info_.tied,
-                 (unsigned long long)open_at_limit_.size(), (int)degenerate, total_cost_[0], d0,
-                 (int)blk_ok_[0]);
-  }
+  if (std::getenv("DYMU_ORDER_DEBUG"))
+    std::fprintf(stderr, "[dymu] early exit: t_closed %.17g band %llu tied %llu open %llu "
+                 "degenerate %d\n", t_closed, (unsigned long long)nb,
+                 (unsigned long long)early_info_.tied, (unsigned long long)open_at_limit_.size(),
+                 (int)degenerate);
   band_cells_ = std::move(band);
   band_unordered_ = band_cells_.size() > 1;
   return nb > 0;
