@@ -275,6 +275,8 @@ class DyMuPathPlanner {
     uint64_t tied = 0, open_at_limit = 0;
     int exact_replay = 0;
     double resolve_ms = 0.0;
+    uint64_t replay_updates = 0;  // reference updates the band replay evaluated
+    int band_exact = 1;           // 0: the replay hit kReplayBudget (values partly the engine's)
   };
   const EarlyExitInfo& lastEarlyExitInfo() const { return early_info_; }
   // Engine options (device ordinal etc.); takes effect on the next solve.
@@ -330,6 +332,7 @@ class DyMuPathPlanner {
   // the reference's early exit replayed exactly on the host (degenerate ties only)
   bool exactEarlyExit(unsigned si, unsigned sj);
   static constexpr uint64_t kExactReplayCells = 1ull << 24;
+  static constexpr uint64_t kReplayBudget = 1ull << 26;  // band-replay updates per exit
   // band_cells_ into the reference's insertion order, if still in grid order
   void orderBand();
   bool safeNode(unsigned i, unsigned j) const;

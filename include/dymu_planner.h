@@ -78,8 +78,10 @@ int64_t dymu_planner_last_band_size(dymu_planner* p);
 int dymu_planner_last_stats(dymu_planner* p, dymu_stats* out);
 /* the last computeTotalCostMap's exit-order resolution: out[0] cells
  * of exactly the exit value, out[1] how many of them the reference had not closed,
- * out[2] 1 if the exact host replay ran (degenerate ties only), out[3] host ms */
-int dymu_planner_last_early_exit(dymu_planner* p, double out[4]);
+ * out[2] 1 if the exact host replay ran (degenerate ties only), out[3] host ms,
+ * out[4] reference updates the band replay evaluated, out[5] 1 if every band value
+ * is the reference's (0: the replay hit its work bound) */
+int dymu_planner_last_early_exit(dymu_planner* p, double out[6]);
 /* how the last solve ran: 0 cold, 1 windowed re-propagation from the window
  * where the speed changed (dymu_resolve_window), 2 previous map reused */
 int dymu_planner_last_solve_kind(dymu_planner* p);

@@ -760,6 +760,8 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
       std::sort(open_at_limit_.begin(), open_at_limit_.end());
     }
   }
+  const double ms_order =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   // the band with the cells the reference left OPEN at t_closed: they join it, and
   // a neighbour of theirs stays in it only if it has another CLOSED neighbour
   // (otherwise it was never reached: +inf)
@@ -839,9 +841,10 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
   }
   if (std::getenv("DYMU_ORDER_DEBUG"))
     std::fprintf(stderr, "[dymu] early exit: t_closed %.17g band %llu tied %llu open %llu "
-                 "degenerate %d\n", t_closed, (unsigned long long)nb,
-                 (unsigned long long)early_info_.tied, (unsigned long long)open_at_limit_.size(),
-                 (int)degenerate);
+                 "degenerate %d, %.1f ms order + %.1f ms band\n", t_closed,
+                 (unsigned long long)nb, (unsigned long long)early_info_.tied,
+                 (unsigned long long)open_at_limit_.size(), (int)degenerate, ms_order,
+                 early_info_.resolve_ms - ms_order);
   band_cells_ = std::move(band);
   band_unordered_ = band_cells_.size() > 1;
   return nb > 0;
@@ -863,27 +866,71 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
 // undetermined (degenerate ties, pop_order.hpp): the values are not to be used.
 bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& band,
                                  std::vector<double>& out) {
-  struct KeyHash {
-    size_t operator()(const std::pair<uint64_t, uint64_t>& k) const {
-      return std::hash<uint64_t>()(k.first * 0x9E3779B97F4A7C15ull ^ k.second);
-    }
-  };
   auto mirror = [this](uint64_t k) { return T(k); };
   using Order = PopOrder<decltype(mirror)>;
+  // open-addressing memo of upd(k, s), keyed k * 4 + s + 1 (0 = empty)
+  struct Memo {
+    std::vector<uint64_t> key;
+    std::vector<double> v;
+    uint64_t n = 0, mask = 0;
+    Memo() : key(1u << 12, 0), v(1u << 12), mask((1u << 12) - 1) {}
+    static uint64_t h(uint64_t x) { return (x * 0x9E3779B97F4A7C15ull) >> 17; }
+    double* find(uint64_t k) {
+      for (uint64_t q = h(k) & mask;; q = (q + 1) & mask) {
+        if (key[q] == k) return &v[q];
+        if (key[q] == 0) return nullptr;
+      }
+    }
+    void put(uint64_t k, double x) {
+      if (2 * (n + 1) > key.size()) grow();
+      uint64_t q = h(k) & mask;
+      while (key[q] != 0 && key[q] != k) q = (q + 1) & mask;
+      if (key[q] == 0) ++n;
+      key[q] = k;
+      v[q] = x;
+    }
+    void grow() {
+      std::vector<uint64_t> ok(key.size() * 2, 0);
+      std::vector<double> ov(key.size() * 2);
+      ok.swap(key);
+      ov.swap(v);
+      mask = key.size() - 1;
+      n = 0;
+      for (size_t q = 0; q < ok.size(); ++q)
+        if (ok[q]) put(ok[q], ov[q]);
+    }
+  };
   struct Replay {
     DyMuPathPlanner& pl;
     Order po;
     const double* F;
     int64_t NX, NY;
-    std::unordered_map<std::pair<uint64_t, uint64_t>, double, KeyHash> memo;
+    uint64_t last;                 // the exit moment
+    double lim;                    // closed_limit_
+    const std::vector<uint64_t>& open;  // open_at_limit_
+    uint64_t budget;               // upd evaluations left before giving up
+    Memo memo;                     // upd(k, s)
+    std::unordered_map<uint64_t, double> bmemo;  // band values at the exit
+    uint64_t band_k = ~0ull;       // the band cell being evaluated at the exit
+    bool overrun = false;          // the budget or the depth bound was hit
 
     bool in_grid(int64_t i, int64_t j) const { return i >= 0 && j >= 0 && i < NX && j < NY; }
-    // value of (i, j) if it is CLOSED by moment c, else +inf
-    double closed_by(int64_t i, int64_t j, uint64_t c) {
+    double tv(int64_t i, int64_t j) const {  // T(i, j), fetching its block on first use
+      const uint64_t b = (uint64_t)(j >> 7) * pl.nbx_ + (uint64_t)(i >> 7);
+      const uint64_t k = (uint64_t)(j * NX + i);
+      if (pl.blk_missing_ && !pl.blk_ok_[b]) return pl.T(k);
+      return pl.total_cost_[k];
+    }
+    bool closed(uint64_t k, double t) const {  // closedCell with T already loaded
+      if (!(t < kInf) || t > lim) return false;
+      return t < lim || open.empty() || !std::binary_search(open.begin(), open.end(), k);
+    }
+    // value of (i, j) if it is CLOSED by moment c (value tc), else +inf
+    double closed_by(int64_t i, int64_t j, uint64_t c, double tc) {
       if (!in_grid(i, j)) return kInf;
       const uint64_t k = (uint64_t)(j * NX + i);
-      if (!pl.closedCell(k)) return kInf;
-      const double t = pl.T(k), tc = pl.T(c);
+      const double t = tv(i, j);
+      if (!closed(k, t)) return kInf;
       if (t < tc || k == c) return t;
       if (t > tc) return kInf;
       return po.popBefore(k, c) ? t : kInf;
@@ -894,45 +941,91 @@ bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& ban
         return (tx + ty + std::sqrt(2 * (C * C) - (tx - ty) * (tx - ty))) / 2;
       return std::fmin(tx, ty) + C;
     }
-    double axis(int64_t ia, int64_t ja, int64_t ib, int64_t jb, uint64_t m, int depth) {
-      const double a = closed_by(ia, ja, m), b = closed_by(ib, jb, m);
+    double axis(int64_t ia, int64_t ja, int64_t ib, int64_t jb, uint64_t m, double tm,
+                int depth) {
+      const double a = closed_by(ia, ja, m, tm), b = closed_by(ib, jb, m, tm);
       if (a < kInf || b < kInf) return std::fmin(a, b);  // OPEN sides are >= T(m) >= it
-      const double va = in_grid(ia, ja) ? val((uint64_t)(ja * NX + ia), m, depth + 1) : kInf;
-      const double vb = in_grid(ib, jb) ? val((uint64_t)(jb * NX + ib), m, depth + 1) : kInf;
+      const double va = in_grid(ia, ja) ? val(ia, ja, m, tm, depth + 1) : kInf;
+      const double vb = in_grid(ib, jb) ? val(ib, jb, m, tm, depth + 1) : kInf;
       return std::fmin(va, vb);
     }
-    double val(uint64_t k, uint64_t c, int depth) {
-      const double C = F[k];
-      if (!(C < kInf)) return kInf;       // obstacles are never updated
-      if (depth > 20000) return pl.T(k);  // pathological chains: the converged value
-      const auto key = std::make_pair(k, c);
-      auto it = memo.find(key);
-      if (it != memo.end()) return it->second;
-      memo.emplace(key, kInf);
-      const int64_t i = (int64_t)(k % NX), j = (int64_t)(k / NX);
-      double v = kInf;
+    // val(k, c) = min over the nb4 m of k popped by moment c of upd(k, m): the update
+    // of k by m's pop depends on m alone, so it is memoised per (k, m) -- at most four
+    // per cell -- and a value at any moment is a min over at most four of them.  When
+    // every neighbour that updates k before k's own pop (a CLOSED k) or before the exit
+    // (a band k) has been popped by c, the value at c is that final one: T(k), or k's
+    // band value -- which cuts the walk back through the front's history short
+    double val(int64_t i, int64_t j, uint64_t c, double tc, int depth) {
+      const uint64_t k = (uint64_t)(j * NX + i);
+      if (!(F[k] < kInf)) return kInf;  // obstacles are never updated
       const int64_t nb[4][2] = {{i, j - 1}, {i - 1, j}, {i + 1, j}, {i, j + 1}};
-      for (const auto& e : nb) {
-        if (!(closed_by(e[0], e[1], c) < kInf)) continue;  // no pop of it updated k yet
-        const uint64_t m = (uint64_t)(e[1] * NX + e[0]);
-        const double tx = axis(i - 1, j, i + 1, j, m, depth);
-        const double ty = axis(i, j - 1, i, j + 1, m, depth);
-        v = std::fmin(v, eikonal(tx, ty, C));
+      const double tk = tv(i, j);
+      const bool kc = closed(k, tk);
+      bool all = true;
+      double byc[4];
+      for (int s = 0; s < 4; ++s) {
+        byc[s] = closed_by(nb[s][0], nb[s][1], c, tc);
+        if (byc[s] < kInf || !all || !in_grid(nb[s][0], nb[s][1])) continue;
+        // a neighbour not popped by c: does it update k before k's value is final?
+        const uint64_t n = (uint64_t)(nb[s][1] * NX + nb[s][0]);
+        if (kc ? n != k && closed_by(nb[s][0], nb[s][1], k, tk) < kInf
+               : closed(n, tv(nb[s][0], nb[s][1])))
+          all = false;
       }
-      memo[key] = v;
+      if (all && kc) return tk;
+      if (all && k != band_k) return bandval(i, j, depth);
+      double v = kInf;
+      for (int s = 0; s < 4; ++s)
+        if (byc[s] < kInf) v = std::fmin(v, upd(i, j, s, depth));
+      return v;
+    }
+    // a band cell's value at the exit, memoised
+    double bandval(int64_t i, int64_t j, int depth) {
+      const uint64_t k = (uint64_t)(j * NX + i);
+      auto it = bmemo.find(k);
+      if (it != bmemo.end()) return it->second;
+      const uint64_t saved = band_k;
+      band_k = k;
+      const double v = val(i, j, last, tv(last % NX, last / NX), depth + 1);
+      band_k = saved;
+      bmemo.emplace(k, v);
+      return v;
+    }
+    // the reference update of k at the pop of its neighbour in nb4 slot s (:462-465)
+    double upd(int64_t i, int64_t j, int s, int depth) {
+      const uint64_t k = (uint64_t)(j * NX + i);
+      const uint64_t key = k * 4 + (uint64_t)s + 1;
+      if (const double* hit = memo.find(key)) return *hit;
+      if (depth > 3000 || budget == 0) {  // give up (~1 MB of stack): the engine's value, flagged
+        overrun = true;
+        return tv(i, j);
+      }
+      --budget;
+      memo.put(key, kInf);  // (pops only go back in time: never re-entered)
+      const int64_t mi = s == 1 ? i - 1 : s == 2 ? i + 1 : i;
+      const int64_t mj = s == 0 ? j - 1 : s == 3 ? j + 1 : j;
+      const uint64_t m = (uint64_t)(mj * NX + mi);
+      const double tm = tv(mi, mj);
+      const double tx = axis(i - 1, j, i + 1, j, m, tm, depth);
+      const double ty = axis(i, j - 1, i, j + 1, m, tm, depth);
+      const double v = eikonal(tx, ty, F[k]);
+      memo.put(key, v);
       return v;
     }
   } rec{*this, Order(mirror, nx_, ny_, idx(goal_i_, goal_j_)), speed_.data(), (int64_t)nx_,
-        (int64_t)ny_, {}};
+        (int64_t)ny_, last, closed_limit_, open_at_limit_, kReplayBudget, {}, {}};
   out.resize(band.size());
-  for (size_t q = 0; q < band.size(); ++q) out[q] = rec.val(band[q], last, 0);
+  for (size_t q = 0; q < band.size(); ++q)
+    out[q] = rec.bandval((int64_t)(band[q] % nx_), (int64_t)(band[q] / nx_), 0);
+  early_info_.replay_updates = kReplayBudget - rec.budget;
+  early_info_.band_exact = rec.overrun ? 0 : 1;
+  if (rec.overrun)
+    log_warn("computeTotalCostMap: the band replay hit its work bound; some band values are "
+             "the engine's (DESIGN.md s3)");
   if (rec.po.degenerate() && std::getenv("DYMU_ORDER_DEBUG")) {
     const uint64_t k = rec.po.whyCell();
     std::fprintf(stderr, "[dymu] order undetermined: reason %d at (%llu, %llu) T=%.17g\n",
                  rec.po.why(), (unsigned long long)(k % nx_), (unsigned long long)(k / nx_), T(k));
-    for (const int64_t d : {-(int64_t)nx_, (int64_t)-1, (int64_t)1, (int64_t)nx_})
-      std::fprintf(stderr, "[dymu]   nb %lld T=%.17g\n", (long long)((int64_t)k + d),
-                   T((uint64_t)((int64_t)k + d)));
   }
   return rec.po.degenerate();
 }

@@ -203,13 +203,15 @@ int dymu_planner_last_stats(dymu_planner* p, dymu_stats* out) {
   return DYMU_OK;
 }
 
-int dymu_planner_last_early_exit(dymu_planner* p, double out[4]) {
+int dymu_planner_last_early_exit(dymu_planner* p, double out[6]) {
   if (!p || !out) return DYMU_ERR_ARG;
   const auto& e = p->pl.lastEarlyExitInfo();
   out[0] = (double)e.tied;
   out[1] = (double)e.open_at_limit;
   out[2] = (double)e.exact_replay;
   out[3] = e.resolve_ms;
+  out[4] = (double)e.replay_updates;
+  out[5] = (double)e.band_exact;
   return DYMU_OK;
 }
 

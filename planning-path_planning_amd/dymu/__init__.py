@@ -693,10 +693,11 @@ class Planner:
         """How the last computeTotalCostMap resolved the reference's pop order at its
         exit value: tied cells, those left OPEN, whether the exact host replay ran
         (degenerate ties only), host milliseconds of the resolution and band replay."""
-        o = np.zeros(4)
+        o = np.zeros(6)
         _check(self._lib.dymu_planner_last_early_exit(self.h, o))
         return {"tied": int(o[0]), "open_at_limit": int(o[1]), "exact_replay": bool(o[2]),
-                "resolve_ms": float(o[3])}
+                "resolve_ms": float(o[3]), "replay_updates": int(o[4]),
+                "band_exact": bool(o[5])}
 
     def lastStats(self) -> dict:
         st = DymuStats()

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -71,6 +72,19 @@ static int compare(const std::vector<std::vector<double>>& M, const std::vector<
 
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "ok";
+  if (mode == "perf") {  // timing of the exit-order resolution on a constant map (manual)
+    const unsigned N = argc > 2 ? (unsigned)std::atoi(argv[2]) : 1024;
+    DyMuPathPlanner p(1.0, 2.0, 5.0, CONSERVATIVE);
+    p.initGlobalLayer(1.0, 0.5, N, N, {0.0, 0.0});
+    p.setCostMap(std::vector<std::vector<double>>(N, std::vector<double>(N, 1.0)));
+    if (!p.setGoal(wp(N / 2, N / 2))) return 2;
+    const bool r = p.computeTotalCostMap(wp(N * 0.7, N * 0.6));
+    const auto& info = p.lastEarlyExitInfo();
+    std::printf("perf N=%u r=%d band=%llu tied=%llu open=%llu resolve_ms=%.1f\n", N, (int)r,
+                (unsigned long long)p.lastBandSize(), (unsigned long long)info.tied,
+                (unsigned long long)info.open_at_limit, info.resolve_ms);
+    return 0;
+  }
   if (mode == "ties") {
     // constant / two-valued cost: mirror images tie, so which cells of exactly the
     // exit value the reference closed -- and which it reached -- depends on its
