@@ -1226,7 +1226,6 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   __shared__ uint32_t s_pref[kShards + 1];
   __shared__ uint32_t s_hout[kBins];
   __shared__ uint32_t s_nq, s_base, s_next, s_merge;
-  __shared__ uint32_t s_cnt[kShards], s_maxc;  // list shard counts and their max
   __shared__ int s_bstar;
   __shared__ unsigned long long s_visits, s_sweeps, s_minout, s_defer;
   __shared__ unsigned long long s_ek[WPB][4];
@@ -1237,32 +1236,42 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
-  const uint32_t shard = blockIdx.x % kShards;
+  // the shard this workgroup appends to: not the one it draws from (b % kShards) --
+  // with shard b % kShards both ways, each residue class of workgroups would feed itself
+  // and a busy region of the front would stay on 16 workgroups (v36 measured 16x16 tiles
+  // at 464 ms so); (b / kShards + pass) % kShards spreads a class's output over all shards
+  const uint32_t shard = (blockIdx.x / kShards + a.epoch) % kShards;
   unsigned long long* trace = a.trace ? a.trace + (uint64_t)blockIdx.x * kTracePts : nullptr;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   // no deadline: 2^30 ticks (10.7 s) ahead, far beyond any pass
   const uint32_t stop_at = (uint32_t)t_start + (a.sweep_deadline ? a.sweep_deadline : (1u << 30));
   if (trace && tid == 0) trace[0] = t_start;
 
-  // The workgroup's entries (v36): draw j of workgroup b is virtual position
-  // v = b + gridDim.x * j of the list's shards interleaved -- entry v / 16 of shard
-  // (v % 16 + v / 256) % 16, a bijection -- so each workgroup samples every shard
-  // (its share is n / gridDim.x within one, as the strided whole-list mapping gave:
-  // a producer flushes contiguously, so a chunk would hold neighbours of the same
-  // visits, mostly admitted or deferred together) and an entry's address needs no
-  // prefix of the shard counts: each wave's FIRST entry is drawn and loaded before the
-  // prologue barrier, its latency hidden behind wave 0's counter / histogram scan.
-  // Positions past a shard's count are holes, skipped without a load.
+  // The workgroup's entries: with at least kShards workgroups, list shard b % kShards is
+  // drawn by the workgroups b, b + kShards, ... -- workgroup b takes its positions
+  // b / kShards + k * step -- so an entry's address needs no prefix of the shard counts,
+  // and each wave's FIRST entry is drawn and loaded before the prologue barrier, its
+  // latency hidden behind wave 0's counter / histogram scan (v36).  A producer flushes
+  // its queue contiguously, so a contiguous chunk would hold the neighbours of the same
+  // visits (mostly admitted or mostly deferred together); strided, the visits per
+  // workgroup spread around the mean.  Fewer workgroups than shards: every gridDim.x-th
+  // entry of the whole list (prefix sums).
+  const bool pershard = gridDim.x >= (unsigned)kShards;
+  const uint32_t cshard = blockIdx.x % kShards;
+  const uint32_t crank = blockIdx.x / kShards;
+  const uint32_t cstep = (gridDim.x - cshard + kShards - 1) / kShards;
   if (tid == 0) s_next = 0;
   s_hout[tid & (kBins - 1)] = 0u;
   __syncthreads();
   uint32_t j0 = 0;
   if (lane == 0) j0 = atomicAdd(&s_next, 1u);
   j0 = __builtin_amdgcn_readfirstlane(j0);
-  const uint32_t v0 = blockIdx.x + gridDim.x * j0;
-  const uint32_t i0 = v0 / kShards, sh0 = (v0 % kShards + v0 / (kShards * kShards)) % kShards;
-  uint32_t c0 = a.count_in[sh0], ent0 = 0;
-  if (i0 < a.shard_cap) ent0 = a.list_in[(uint64_t)sh0 * a.shard_cap + i0];
+  uint32_t ccount = 0, ent0 = 0;
+  if (pershard) {
+    ccount = a.count_in[cshard];
+    const uint32_t p0 = crank + cstep * j0;
+    if (p0 < a.shard_cap) ent0 = a.list_in[(uint64_t)cshard * a.shard_cap + p0];
+  }
 
   const double delta = *a.delta;
   const double origin_in = *a.base_in;
@@ -1270,11 +1279,6 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   const double inv_delta = 1.0 / delta;
   if (wv == 0) {  // shard prefix counts and the threshold bin (as k_fim_pass_prio)
     uint32_t c = lane < kShards ? a.count_in[lane] : 0u;
-    if (lane < kShards) s_cnt[lane] = c;
-    uint32_t cm = c;
-#pragma unroll
-    for (int o = 1; o < kShards; o <<= 1) cm = max(cm, (uint32_t)__shfl_xor(cm, o));
-    if (lane == 0) s_maxc = cm;
     uint32_t h = 0;
 #pragma unroll
     for (int k = 0; k < kShards; ++k) h += a.hist_in[k * kBins + lane];
@@ -1311,7 +1315,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   }
   // the prefetched entry and count into scalar registers (after the scan's loads issued)
   ent0 = __builtin_amdgcn_readfirstlane(ent0);
-  c0 = __builtin_amdgcn_readfirstlane(c0);
+  ccount = __builtin_amdgcn_readfirstlane(ccount);
   __syncthreads();
   const uint32_t n_active = s_pref[kShards];
   const int bstar = s_bstar;
@@ -1361,7 +1365,6 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   const uint32_t nb = gridDim.x;
   bool first = true;
   if (trace && tid == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
-  const uint32_t vend = kShards * s_maxc;  // virtual positions past every shard's count
   bool drawn0 = true;  // j0 / ent0 not consumed yet
   for (;;) {  // wave-uniform
     uint32_t j = j0;
@@ -1369,18 +1372,18 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       if (lane == 0) j = atomicAdd(&s_next, 1u);
       j = __builtin_amdgcn_readfirstlane(j);
     }
-    const uint32_t v = blockIdx.x + gridDim.x * j;
-    if (v >= vend) break;
-    const uint32_t vi = v / kShards, vs = (v % kShards + v / (kShards * kShards)) % kShards;
     uint32_t ent;
-    if (drawn0) {
-      drawn0 = false;
-      if (vi >= c0) continue;  // a hole
-      ent = ent0;
+    if (pershard) {
+      const uint32_t p = crank + cstep * j;
+      if (p >= ccount) break;
+      ent = drawn0 ? ent0 : a.list_in[(uint64_t)cshard * a.shard_cap + p];
+      ent = __builtin_amdgcn_readfirstlane(ent);
     } else {
-      if (vi >= s_cnt[vs]) continue;  // a hole
-      ent = __builtin_amdgcn_readfirstlane(a.list_in[(uint64_t)vs * a.shard_cap + vi]);
+      const uint32_t e = blockIdx.x + j * nb;
+      if (e >= n_active) break;
+      ent = __builtin_amdgcn_readfirstlane(list_at_wave(a.list_in, a.shard_cap, s_pref, e, lane));
     }
+    drawn0 = false;
     const uint32_t tile = ent & kTileMask;
     const int pbin = (int)(ent >> kPackShift) - 1;  // first-insertion bin, -1: none
     const int tx = (int)(tile % (uint32_t)a.ntx);
