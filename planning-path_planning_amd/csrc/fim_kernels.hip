@@ -1236,11 +1236,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
-  // the shard this workgroup appends to: not the one it draws from (b % kShards) --
-  // with shard b % kShards both ways, each residue class of workgroups would feed itself
-  // and a busy region of the front would stay on 16 workgroups (v36 measured 16x16 tiles
-  // at 464 ms so); (b / kShards + pass) % kShards spreads a class's output over all shards
-  const uint32_t shard = (blockIdx.x / kShards + a.epoch) % kShards;
+  const uint32_t shard = blockIdx.x % kShards;
   unsigned long long* trace = a.trace ? a.trace + (uint64_t)blockIdx.x * kTracePts : nullptr;
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   // no deadline: 2^30 ticks (10.7 s) ahead, far beyond any pass
