@@ -4,8 +4,9 @@ as the solve), on CPU:
   * a >= 1024-row readback (getTotalCostMatrix's chunked download) whose device
     copy fails WITHOUT an error text must throw, not return stale rows;
   * setEngineOptions after a solve keeps the solved map readable (map + path);
-  * computeTotalCostMap's early exit on a constant-cost map (every distance ties)
-    finishes with exact CLOSED values (the band replay's tie cycles).
+  * computeTotalCostMap's early exit on constant / two-valued maps (mirror images tie):
+    the whole exit state -- matrix, node states, the band in insertion order -- equals the
+    oracle's bit for bit without the exact host replay (also under ASan / UBSan).
 Never part of the product: the product links the HIP engine, which has no CPU path."""
 import os
 import shutil
@@ -68,3 +69,29 @@ def test_engine_options_after_solve_keep_map(driver):
 def test_early_exit_with_ties(driver):
     r = _run(driver, "ties")
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_early_exit_with_ties_sanitized(tmp_path):
+    """The same exit-order resolution and band replay (csrc/pop_order.hpp, replayBand)
+    under AddressSanitizer + UndefinedBehaviorSanitizer."""
+    if shutil.which("g++") is None:
+        pytest.skip("needs gcc/g++")
+    san = ["-g", "-O1", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+           "-fno-omit-frame-pointer", "-ffp-contract=off", "-pthread"]
+    inc = ["-I" + os.path.join(ROOT, p) for p in ("include", "oracle",
+                                                 "planning-path_planning_amd/csrc")]
+    objs = []
+    for src in ("oracle/oracle.c", "tests/hostengine/host_engine.c"):
+        o = str(tmp_path / (os.path.basename(src) + ".o"))
+        subprocess.run(["gcc", *san, "-std=gnu11", *inc, "-c", os.path.join(ROOT, src), "-o", o],
+                       check=True)
+        objs.append(o)
+    exe = str(tmp_path / "driver_san")
+    srcs = [os.path.join(ROOT, s) for s in (
+        "tests/hostengine/driver.cpp", "planning-path_planning_amd/csrc/planner.cpp",
+        "planning-path_planning_amd/csrc/local_layer.cpp")]
+    subprocess.run(["g++", *san, "-std=c++17", *inc, *srcs, *objs, "-o", exe, "-lm"], check=True)
+    r = _run(exe, "ties", ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:verify_asan_link_order=0",
+             UBSAN_OPTIONS="print_stacktrace=1")
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
