@@ -1243,32 +1243,6 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   const uint32_t stop_at = (uint32_t)t_start + (a.sweep_deadline ? a.sweep_deadline : (1u << 30));
   if (trace && tid == 0) trace[0] = t_start;
 
-  // The workgroup's entries: with at least kShards workgroups, list shard b % kShards is
-  // drawn by the workgroups b, b + kShards, ... -- workgroup b takes its positions
-  // b / kShards + k * step -- so an entry's address needs no prefix of the shard counts,
-  // and each wave's FIRST entry is drawn and loaded before the prologue barrier, its
-  // latency hidden behind wave 0's counter / histogram scan (v36).  A producer flushes
-  // its queue contiguously, so a contiguous chunk would hold the neighbours of the same
-  // visits (mostly admitted or mostly deferred together); strided, the visits per
-  // workgroup spread around the mean.  Fewer workgroups than shards: every gridDim.x-th
-  // entry of the whole list (prefix sums).
-  const bool pershard = gridDim.x >= (unsigned)kShards;
-  const uint32_t cshard = blockIdx.x % kShards;
-  const uint32_t crank = blockIdx.x / kShards;
-  const uint32_t cstep = (gridDim.x - cshard + kShards - 1) / kShards;
-  if (tid == 0) s_next = 0;
-  s_hout[tid & (kBins - 1)] = 0u;
-  __syncthreads();
-  uint32_t j0 = 0;
-  if (lane == 0) j0 = atomicAdd(&s_next, 1u);
-  j0 = __builtin_amdgcn_readfirstlane(j0);
-  uint32_t ccount = 0, ent0 = 0;
-  if (pershard) {
-    ccount = a.count_in[cshard];
-    const uint32_t p0 = crank + cstep * j0;
-    if (p0 < a.shard_cap) ent0 = a.list_in[(uint64_t)cshard * a.shard_cap + p0];
-  }
-
   const double delta = *a.delta;
   const double origin_in = *a.base_in;
   const double origin_out = bitsd(*a.minkey_in);
@@ -1300,6 +1274,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       s_pref[0] = 0u;
       s_bstar = (a.target > 0 && n > target && m) ? (int)__ffsll((long long)m) - 1 : kBins;
       s_nq = 0;
+      s_next = 0;
       s_merge = 0;
       s_visits = 0;
       s_sweeps = 0;
@@ -1309,9 +1284,7 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
       s_psmin = 0u;
     }
   }
-  // the prefetched entry and count into scalar registers (after the scan's loads issued)
-  ent0 = __builtin_amdgcn_readfirstlane(ent0);
-  ccount = __builtin_amdgcn_readfirstlane(ccount);
+  s_hout[tid & (kBins - 1)] = 0u;
   __syncthreads();
   const uint32_t n_active = s_pref[kShards];
   const int bstar = s_bstar;
@@ -1358,28 +1331,21 @@ __global__ __launch_bounds__(64 * WPB, 4) void k_fim_pass_dyn(PassArgs a) {
   uint32_t my_cd = 0, my_cap = 0, my_dl = 0, my_rmax = 0, my_rmin = ~0u;  // a.pstat only
   double* img = s_img[wv];
   unsigned long long* ek = s_ek[wv];
+  // the workgroup's entries are every gridDim.x-th of the list from its own index, not
+  // a contiguous chunk: a producer flushes its queue contiguously, so a chunk holds
+  // neighbours of the same visits -- mostly admitted or mostly deferred together -- and
+  // a workgroup with more visits than waves ends the pass late; strided, the visits
+  // per workgroup spread binomially around the mean
   const uint32_t nb = gridDim.x;
   bool first = true;
   if (trace && tid == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
-  bool drawn0 = true;  // j0 / ent0 not consumed yet
   for (;;) {  // wave-uniform
-    uint32_t j = j0;
-    if (!drawn0) {
-      if (lane == 0) j = atomicAdd(&s_next, 1u);
-      j = __builtin_amdgcn_readfirstlane(j);
-    }
-    uint32_t ent;
-    if (pershard) {
-      const uint32_t p = crank + cstep * j;
-      if (p >= ccount) break;
-      ent = drawn0 ? ent0 : a.list_in[(uint64_t)cshard * a.shard_cap + p];
-      ent = __builtin_amdgcn_readfirstlane(ent);
-    } else {
-      const uint32_t e = blockIdx.x + j * nb;
-      if (e >= n_active) break;
-      ent = __builtin_amdgcn_readfirstlane(list_at_wave(a.list_in, a.shard_cap, s_pref, e, lane));
-    }
-    drawn0 = false;
+    uint32_t e = 0;
+    if (lane == 0) e = blockIdx.x + atomicAdd(&s_next, 1u) * nb;
+    e = __builtin_amdgcn_readfirstlane(e);
+    if (e >= n_active) break;
+    const uint32_t ent =
+        __builtin_amdgcn_readfirstlane(list_at_wave(a.list_in, a.shard_cap, s_pref, e, lane));
     const uint32_t tile = ent & kTileMask;
     const int pbin = (int)(ent >> kPackShift) - 1;  // first-insertion bin, -1: none
     const int tx = (int)(tile % (uint32_t)a.ntx);
