@@ -257,7 +257,8 @@ def test_config1_exact_call(dymu, oracle, inputs):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("N,g,s", [(160, (80, 80), (20, 140)), (512, (256, 256), (102, 128)),
-                                   (96, (48, 48), (48, 20)), (2048, (1024, 1024), (200, 1900))])
+                                   (96, (48, 48), (48, 20)), (2048, (1024, 1024), (200, 1900)),
+                                   (4096, (2048, 2048), (2867, 2457))])  # a 1:2 staircase front
 def test_early_exit_ties_exact(dymu, oracle, N, g, s):
     """computeTotalCostMap on a constant-speed map, where every mirror image ties:
     which of the cells of exactly the exit value the reference closed, and so which
