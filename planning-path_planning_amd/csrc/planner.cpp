@@ -758,6 +758,9 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
       for (const uint64_t x : eq)
         if (x != last && po.popBefore(last, x)) open_at_limit_.push_back(x);
       std::sort(open_at_limit_.begin(), open_at_limit_.end());
+      // an undetermined order (pop_order.hpp) leaves every tied cell CLOSED, as the
+      // engine's state has it; the exact host replay below takes over where it may
+      if (po.degenerate()) open_at_limit_.clear();
     }
   }
   const double ms_order =
@@ -837,7 +840,6 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
     }
     log_warn("computeTotalCostMap: degenerate ties at the exit value; the pop order among "
              "them is not reproduced (grid larger than the exact-replay limit)");
-    open_at_limit_.clear();
   }
   if (std::getenv("DYMU_ORDER_DEBUG"))
     std::fprintf(stderr, "[dymu] early exit: t_closed %.17g band %llu tied %llu open %llu "
@@ -916,12 +918,13 @@ bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& ban
 
     bool in_grid(int64_t i, int64_t j) const { return i >= 0 && j >= 0 && i < NX && j < NY; }
     double tv(int64_t i, int64_t j) const {  // T(i, j), fetching its block on first use
-      const uint64_t b = (uint64_t)(j >> 7) * pl.nbx_ + (uint64_t)(i >> 7);
+      const uint64_t b = (uint64_t)(j / kBlk) * pl.nbx_ + (uint64_t)(i / kBlk);
       const uint64_t k = (uint64_t)(j * NX + i);
       if (pl.blk_missing_ && !pl.blk_ok_[b]) return pl.T(k);
       return pl.total_cost_[k];
     }
-    bool closed(uint64_t k, double t) const {  // closedCell with T already loaded
+    // closedCell with T already loaded (node_state_ is empty here: propagate cleared it)
+    bool closed(uint64_t k, double t) const {
       if (!(t < kInf) || t > lim) return false;
       return t < lim || open.empty() || !std::binary_search(open.begin(), open.end(), k);
     }
