@@ -28,7 +28,8 @@
 //     are final: CLOSED cells hold their converged values, the
 //     narrow band the reference's tentative values (replayed on the host from
 //     the CLOSED values), every other cell +inf; ties between equal total
-//     costs may order differently from the reference's insertion order.
+//     costs follow the reference's insertion order, rebuilt from the values
+//     (csrc/pop_order.hpp), and so does the band list.
 //   * the node-pointer members are accessors returning snapshots:
 //     globalNarrowband(), globalPropagatedNodes(), globalGoal(), localAgent(),
 //     localNarrowband(), localExpandableObstacles(), localPropagatedNodes(); a
