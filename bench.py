@@ -74,6 +74,10 @@ def parse():
                     help="run the row-slab path even at N=1 (exercises the RCCL code path)")
     ap.add_argument("--cpu-linear-size", type=int, default=2048,
                     help="edge of the grid the reference's linear-scan band is timed on")
+    ap.add_argument("--sustain-s", type=float, default=8.0,
+                    help="after the timed steps, keep solving for this many seconds (not "
+                         "timed into `value`): the sustained rate and its spread, and a GPU "
+                         "busy long enough for an outside sampler to see; 0 = off")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the exact-sqrt / deterministic re-runs of the headline solve")
     ap.add_argument("--no-parity", action="store_true",
@@ -266,6 +270,19 @@ def run_single(args):
     eng.set_profiling(False)
     T = np.empty(2)
     eng.d2h(T, dT)  # touch the result
+    if args.sustain_s > 0:  # untimed for `value`: the same solve back to back
+        per = []
+        t1 = time.perf_counter()
+        while time.perf_counter() - t1 < args.sustain_s:
+            t2 = time.perf_counter()
+            eng.solve_device(dF, dT, N, N, N, g[0], g[1])
+            per.append((time.perf_counter() - t2) * 1e3)
+        per.sort()
+        tot["sustained"] = {"seconds": round(time.perf_counter() - t1, 2), "steps": len(per),
+                            "ms_per_step_median": round(per[len(per) // 2], 3),
+                            "ms_per_step_min": round(per[0], 3),
+                            "ms_per_step_max": round(per[-1], 3),
+                            "note": "back-to-back solves after the timed region (not in value)"}
     if getattr(args, "keep_result", False):  # the last timed solve's map, for oracle parity
         tot["T"] = np.empty((N, N))
         eng.d2h(tot["T"], dT)
@@ -494,6 +511,8 @@ def main():
         line["config"]["transports_dropped"] = tot["transports_dropped"]
     if tot.get("variants"):
         line["variants"] = tot["variants"]
+    if tot.get("sustained"):
+        line["sustained"] = tot["sustained"]
     if tot.get("parity") is not None:  # the sharded run's self-check (bench_sharded.self_check)
         line["parity"] = tot["parity"]
     if args.fake_cpu:
