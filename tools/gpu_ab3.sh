@@ -11,7 +11,7 @@ for i in $(seq 1 ${PAIRS:-3}); do
   for v in new base; do
     if [ $v = base ]; then export DYMU_LIBDIR=$GRAFT_REPO_ROOT/ab/$BASE/lib; else unset DYMU_LIBDIR; fi
     if [ $v = new ]; then ENVV="${NEW_ENV:-X_=0}"; else ENVV="X_=0"; fi
-    env $ENVV timeout -k 10 300 python -u bench.py --no-planner --no-variants --cpu-sample 0 --steps 20 --warmup 3 > $O/bench_$v$i.log 2>&1 || { tail -20 $O/bench_$v$i.log; exit 1; }
+    env $ENVV timeout -k 10 300 python -u bench.py --no-planner --no-variants --cpu-sample 0 --sustain-s 0 --steps 20 --warmup 3 > $O/bench_$v$i.log 2>&1 || { tail -20 $O/bench_$v$i.log; exit 1; }
     python3 -c "import json; d=json.loads(open('$O/bench_$v$i.log').read().strip().splitlines()[-1]); print('$v$i', d['ms_per_step'], d['config']['passes_per_solve'], d['config']['tile_visits_per_solve'], d['config']['inner_sweeps_per_solve'], d['roofline']['avg_launch_us'])"
   done
 done
