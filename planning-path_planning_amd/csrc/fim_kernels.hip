@@ -24,12 +24,6 @@
 namespace dymu {
 
 __device__ __forceinline__ double dinf() { return __builtin_inf(); }
-// Pass-kernel write-back: an agent-scope relaxed store is write-through (the
-// line leaves the XCD's L2 while the kernel runs), so the end-of-pass release
-// has fewer dirty bytes to flush before the next pass may start.
-__device__ __forceinline__ void wt_store(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // fmin for operands that are never NaN (T values are >= 0 or +inf): a plain
 // compare-select, so the compiler does not canonicalise both inputs first.
@@ -978,8 +972,8 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const bool cr_ = tr[k] < tr0[k], cb_ = tb[k] < tb0[k];
-    if (cr_) wt_store(&a.T[gj * a.ld + i0 + cr[k]], tr[k]);
-    if (cb_) wt_store(&a.T[gj * a.ld + i0 + cb[k]], tb[k]);
+    if (cr_) a.T[gj * a.ld + i0 + cr[k]] = tr[k];
+    if (cb_) a.T[gj * a.ld + i0 + cb[k]] = tb[k];
     dr[k] = cr_ ? tr[k] : dinf();
     db[k] = cb_ ? tb[k] : dinf();
   }
@@ -998,7 +992,7 @@ __device__ __forceinline__ int visit16(const PassArgs& a, double* img, unsigned 
   }
   if (q == 0 || q == 3) {  // W / E edge: column 0 (cr[0] or cb[0]) / column 15 (cr[1] or cb[1])
     const double c = q == 0 ? (odd ? db[0] : dr[0]) : (odd ? dr[1] : db[1]);
-    if (c < dinf()) wt_store(&a.ec[((uint64_t)ty * (uint64_t)a.ntx + (uint64_t)tx) * 32 + (q == 0 ? 0 : 16) + r], c);
+    if (c < dinf()) a.ec[((uint64_t)ty * (uint64_t)a.ntx + (uint64_t)tx) * 32 + (q == 0 ? 0 : 16) + r] = c;
     const double m = across(c, img[q == 0 ? rb - 1 : rb + TT]);
     if (m < dinf()) atomicMin(&ek[q == 0 ? 1 : 2], dbits(m));
   }
