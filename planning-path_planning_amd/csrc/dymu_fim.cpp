@@ -86,7 +86,10 @@ struct dymu_ctx {
   unsigned long long* h_probe = nullptr;  // pinned [2]: early-exit probe (max T, min key)
   uint64_t* d_band = nullptr;   // early-exit band indices (device)
   uint64_t band_cap = 0;
-  void* d_xfer = nullptr;       // staging of dymu_find_equal / dymu_scatter (device)
+  // dymu_find_equal / dymu_scatter exchange indices and values through this pinned,
+  // host-coherent, device-mapped buffer, which their kernels read and write in place
+  void* h_xfer = nullptr;       // host address
+  void* d_xfer = nullptr;       // its device address
   uint64_t xfer_cap = 0;        // bytes
   unsigned long long* d_scratch = nullptr;  // 8 words of per-call device scalars
   double* d_lut = nullptr;      // computeCostMap LUT (device copy)
@@ -188,14 +191,23 @@ int ensure_prio(dymu_ctx* c, uint32_t ntiles) {
   return DYMU_OK;
 }
 
+// The transfer buffer of dymu_find_equal / dymu_scatter: pinned host memory the
+// kernels access in place, so no copy command stands between the host's data and
+// the kernel.  Round 5's version staged through hipMallocAsync memory with copies; on
+// this stack (ROCm 7.2, gfx950) a stream-ordered pool allocation is not seen alike by
+// the copy paths and the kernels beyond its first 4 KiB page -- a kernel read an
+// earlier allocation's bytes, whatever the copy's source, synchronicity or ordering
+// (tools/copy_order_probe.hip, profiles/r06/copy_order_probe.jsonl).
+// Callers synchronise the stream before the buffer is rewritten.
 int ensure_xfer(dymu_ctx* c, uint64_t bytes) {
   if (bytes <= c->xfer_cap) return DYMU_OK;
-  if (c->d_xfer) HIPC(c, hipFree(c->d_xfer));
-  c->d_xfer = nullptr;
+  if (c->h_xfer) HIPC(c, hipHostFree(c->h_xfer));
+  c->h_xfer = c->d_xfer = nullptr;
   c->xfer_cap = 0;
   bytes = std::max<uint64_t>(bytes, 1u << 16);
-  HIPC(c, hipMalloc(&c->d_xfer, bytes));
+  HIPC(c, hipHostMalloc(&c->h_xfer, bytes, hipHostMallocCoherent | hipHostMallocMapped));
   c->xfer_cap = bytes;
+  HIPC(c, hipHostGetDevicePointer(&c->d_xfer, c->h_xfer, 0));
   return DYMU_OK;
 }
 
@@ -960,8 +972,7 @@ int resolve_core(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_
   const uint32_t wi1 = (uint32_t)std::min<uint64_t>((uint64_t)i0 + w + 1, nx);
   const uint32_t wj1 = (uint32_t)std::min<uint64_t>((uint64_t)j0 + h + 1, ny);
   unsigned long long* theta = c->d_scratch;
-  const unsigned long long inf_bits = 0x7FF0000000000000ull;
-  HIPC(c, hipMemcpyAsync(theta, &inf_bits, sizeof inf_bits, hipMemcpyHostToDevice, st));
+  HIPC(c, launch_store_u64(theta, 0x7FF0000000000000ull, st));  // +inf bits
   HIPC(c, launch_window_min(dT, (int64_t)ld, wi0, wj0, wi1, wj1, theta, st));
   UpdateArgs u{};
   u.T = dT;
@@ -1217,7 +1228,7 @@ int dymu_destroy(dymu_ctx* c) {
   if (c->h_probe) (void)hipHostFree(c->h_probe);
   if (c->h_mail) (void)hipHostFree(c->h_mail);
   if (c->d_band) (void)hipFree(c->d_band);
-  if (c->d_xfer) (void)hipFree(c->d_xfer);
+  if (c->h_xfer) (void)hipHostFree(c->h_xfer);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return DYMU_OK;
@@ -1304,9 +1315,10 @@ int dymu_find_equal(dymu_ctx* c, const double* dT, uint32_t nx, uint32_t ny, uin
   if (!c || !dT || !count || ld < nx || (cap && !idx)) return DYMU_ERR_ARG;
   HIPC(c, hipSetDevice(c->device));
   hipStream_t st = pick_stream(c, stream);
+  HIPC(c, hipStreamSynchronize(st));  // no earlier kernel still uses the transfer buffer
   int rc = ensure_xfer(c, sizeof(uint64_t) * (cap ? cap : 1));
   if (rc) return rc;
-  uint64_t* di = static_cast<uint64_t*>(c->d_xfer);
+  uint64_t* di = static_cast<uint64_t*>(c->d_xfer);  // written by the kernel in host memory
   unsigned long long* cnt = c->d_scratch + 4;
   HIPC(c, hipMemsetAsync(cnt, 0, sizeof(unsigned long long), st));
   HIPC(c, launch_count_equal(dT, (int64_t)ld, nx, ny, value, cnt, di, cap, st));
@@ -1314,7 +1326,7 @@ int dymu_find_equal(dymu_ctx* c, const double* dT, uint32_t nx, uint32_t ny, uin
   HIPC(c, hipStreamSynchronize(st));
   *count = c->h_probe[0];
   const uint64_t m = std::min<uint64_t>(*count, cap);
-  if (m) HIPC(c, hipMemcpy(idx, di, sizeof(uint64_t) * m, hipMemcpyDeviceToHost));
+  if (m) std::memcpy(idx, c->h_xfer, sizeof(uint64_t) * m);
   return DYMU_OK;
 }
 
@@ -1324,17 +1336,15 @@ int dymu_scatter(dymu_ctx* c, double* dT, uint32_t nx, uint64_t ld, const uint64
   if (n == 0) return DYMU_OK;
   HIPC(c, hipSetDevice(c->device));
   hipStream_t st = pick_stream(c, stream);
-  // a context-owned staging buffer and blocking copies: the stream-ordered pool
-  // allocation with asynchronous pageable copies this replaced delivered zeros to the
-  // kernel after an earlier free in the same stream (round 5: the early exit wrote
-  // T = 0 into cell 0)
+  // indices and values written into the pinned transfer buffer on the host and read
+  // there by the kernel (ensure_xfer): no copy command, no device staging
+  HIPC(c, hipStreamSynchronize(st));  // no earlier kernel still uses the transfer buffer
   int rc = ensure_xfer(c, (sizeof(uint64_t) + sizeof(double)) * n);
   if (rc) return rc;
-  uint64_t* di = static_cast<uint64_t*>(c->d_xfer);
-  double* dv = reinterpret_cast<double*>(di + n);
-  HIPC(c, hipStreamSynchronize(st));
-  HIPC(c, hipMemcpy(di, idx, sizeof(uint64_t) * n, hipMemcpyHostToDevice));
-  HIPC(c, hipMemcpy(dv, vals, sizeof(double) * n, hipMemcpyHostToDevice));
+  std::memcpy(c->h_xfer, idx, sizeof(uint64_t) * n);
+  std::memcpy(static_cast<char*>(c->h_xfer) + sizeof(uint64_t) * n, vals, sizeof(double) * n);
+  const uint64_t* di = static_cast<const uint64_t*>(c->d_xfer);
+  const double* dv = reinterpret_cast<const double*>(di + n);
   HIPC(c, launch_scatter(dT, (int64_t)ld, nx, di, dv, n, st));
   HIPC(c, hipStreamSynchronize(st));
   return DYMU_OK;

@@ -284,6 +284,8 @@ hipError_t launch_probe(const double* T, int64_t ld, const ProbeCells& cells,
 hipError_t launch_early_mask(const double* F, double* T, int64_t ld, uint32_t nx, uint32_t ny,
                              double t_closed, uint64_t* band, unsigned long long* n_band,
                              uint64_t cap, hipStream_t st);
+// *p = v, in stream order (no host-to-device copy for a per-call scalar)
+hipError_t launch_store_u64(unsigned long long* p, unsigned long long v, hipStream_t st);
 // T[(idx / nx) * ld + idx % nx] = vals[k]
 hipError_t launch_scatter(double* T, int64_t ld, uint32_t nx, const uint64_t* idx,
                           const double* vals, uint64_t n, hipStream_t st);

@@ -332,6 +332,11 @@ __global__ void k_early_mask(const double* F, double* T, int64_t ld, uint32_t nx
   }
 }
 
+// *p = v (a per-call device scalar initialised in stream order, without a host copy)
+__global__ void k_store_u64(unsigned long long* p, unsigned long long v) {
+  if (threadIdx.x == 0) *p = v;
+}
+
 __global__ void k_scatter(double* T, int64_t ld, uint32_t nx, const uint64_t* idx,
                           const double* vals, uint64_t n) {
   for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
@@ -367,6 +372,11 @@ hipError_t launch_scatter(double* T, int64_t ld, uint32_t nx, const uint64_t* id
   if (b > 4096) b = 4096;
   if (b == 0) return hipSuccess;
   hipLaunchKernelGGL(k_scatter, dim3((unsigned)b), dim3(256), 0, st, T, ld, nx, idx, vals, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_store_u64(unsigned long long* p, unsigned long long v, hipStream_t st) {
+  hipLaunchKernelGGL(k_store_u64, dim3(1), dim3(64), 0, st, p, v);
   return hipGetLastError();
 }
 

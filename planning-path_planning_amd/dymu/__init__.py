@@ -309,6 +309,24 @@ class Engine:
         _check(self._lib.dymu_synth_speed(self.ctx, dF, nx, ny, ld, row0, seed, obst_frac,
                                           obst_seed, goal_i, goal_j, stream or None), self.ctx)
 
+    def find_equal(self, dT: int, nx: int, ny: int, ld: int, value: float, cap: int):
+        """Cells whose value is bitwise `value` (dymu_find_equal): (count, indices of the
+        first min(count, cap) of them, j * nx + i, in no particular order)."""
+        idx = np.zeros(max(1, cap), dtype=np.uint64)
+        n = _u64()
+        _check(self._lib.dymu_find_equal(self.ctx, dT, nx, ny, ld, float(value), idx.ctypes.data,
+                                         cap, ctypes.byref(n), None), self.ctx)
+        return n.value, idx[:min(n.value, cap)]
+
+    def scatter(self, dT: int, nx: int, ld: int, idx: np.ndarray, vals: np.ndarray):
+        """T[idx // nx, idx % nx] = vals on the device (dymu_scatter)."""
+        idx = np.ascontiguousarray(idx, dtype=np.uint64)
+        vals = np.ascontiguousarray(vals, dtype=np.float64)
+        if idx.shape != vals.shape:
+            raise ValueError("idx and vals differ in shape")
+        _check(self._lib.dymu_scatter(self.ctx, dT, nx, ld, idx.ctypes.data, vals.ctypes.data,
+                                      idx.size, None), self.ctx)
+
     def alloc(self, nbytes: int) -> int:
         p = _vp()
         _check(self._lib.dymu_device_alloc(self.ctx, nbytes, ctypes.byref(p)), self.ctx)
