@@ -46,6 +46,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <optional>
 #include <string>
 #include <vector>
@@ -93,6 +94,7 @@ struct localNode {
 
 struct LocalLayer;  // csrc/local_layer.hpp
 struct PathIndex;   // csrc/local_layer.hpp
+struct TieGuard;    // csrc/pop_order.hpp
 
 class DyMuPathPlanner {
  public:
@@ -171,11 +173,14 @@ class DyMuPathPlanner {
   // the reference's public globalNode::state written by a caller (its FMM loop sets
   // CLOSED after each minCostGlobalNode); the next solve recomputes every state
   void setGlobalNodeState(unsigned i, unsigned j, node_state s);
-  // global_propagated_nodes (:447): every node with a finite total cost -- grid-index
-  // order, then those added by propagateGlobalNode in insertion order.  (At 16384^2
+  // global_propagated_nodes (:447): every node with a finite total cost in the
+  // reference's insertion order, then those added by propagateGlobalNode.  (At 16384^2
   // after a full solve that is ~2.6e8 snapshots: globalPropagatedCount first.)
   std::vector<globalNode> globalPropagatedNodes();
   uint64_t globalPropagatedCount();
+  // every node's state (ny*nx, row-major: 1 CLOSED, 0 OPEN) as the last solve or the
+  // caller's setGlobalNodeState left it (the reference's globalNode::state, in bulk)
+  void copyNodeStates(uint8_t* out);
   // :731-784 / L:979-1023: the normalised descent direction at a node (the
   // reference's gradientNode(globalNode*) / gradientNode(localNode*))
   void gradientNode(unsigned i, unsigned j, double& dnx, double& dny) const;
@@ -274,10 +279,14 @@ class DyMuPathPlanner {
   // ties only), host time of the resolution and band replay.
   struct EarlyExitInfo {
     uint64_t tied = 0, open_at_limit = 0;
-    int exact_replay = 0;
+    int exact_replay = 0;         // 1: the exit was replayed exactly on the host
     double resolve_ms = 0.0;
     uint64_t replay_updates = 0;  // reference updates the band replay evaluated
-    int band_exact = 1;           // 0: the replay hit kReplayBudget (values partly the engine's)
+    int band_exact = 1;           // every band value is the reference's (always, since round 6)
+    // comparisons of engine values rounding could flip (near ties, pop_order.hpp's
+    // TieGuard): any sends the exit to the exact host replay
+    uint64_t near_ties = 0;
+    unsigned replay_threads = 0;  // host threads of the band replay
   };
   const EarlyExitInfo& lastEarlyExitInfo() const { return early_info_; }
   // Engine options (device ordinal etc.); takes effect on the next solve.
@@ -327,13 +336,42 @@ class DyMuPathPlanner {
   template <class ERows, class TRows>
   bool costMapFromRows(const ERows& elev_row, const TRows& terr_row);
   bool propagate(bool early, unsigned si, unsigned sj);
-  // the band's tentative values at the moment `last` was popped; true when the
-  // reference's pop order was undetermined (degenerate ties): out is then unusable
-  bool replayBand(uint64_t last, const std::vector<uint64_t>& band, std::vector<double>& out);
-  // the reference's early exit replayed exactly on the host (degenerate ties only)
-  bool exactEarlyExit(unsigned si, unsigned sj);
-  static constexpr uint64_t kExactReplayCells = 1ull << 24;
+  // the band's tentative values at the moment `last` was popped; true when they are
+  // not to be used: the reference's pop order was undetermined or near-tied (guard),
+  // or the replay hit its work bound
+  bool replayBand(uint64_t last, const std::vector<uint64_t>& band, std::vector<double>& out,
+                  TieGuard& guard);
+  // the reference's early exit replayed exactly on the host over the region box
+  // (inclusive; empty: the whole grid) -- when the values cannot decide the exit
+  bool exactEarlyExit(unsigned si, unsigned sj, const int64_t box[4]);
+  // the reference FMM on the host (exact): until (si, sj) and its nb4 are CLOSED, or
+  // the band empties for si < 0; over a box (inclusive, grown to the grid if short)
+  struct HostFmm {
+    int64_t bx[4], W = 0;
+    std::vector<double> T;        // box-local, row pitch W
+    std::vector<uint8_t> st;      // 1 CLOSED, 2 in the band
+    std::vector<uint64_t> order;  // grid indices, in first-insertion order
+    uint64_t band = 0;
+  };
+  HostFmm hostFmm(int64_t si, int64_t sj, const int64_t box[4]) const;
+  // global_propagated_nodes' order after a GPU solve (reference insertion order)
+  std::vector<uint64_t> insertionOrder();
+  bool have_start_ = false;  // the last early exit's start and region (exact fallback)
+  unsigned start_i_ = 0, start_j_ = 0;
+  int64_t exit_box_[4] = {0, 0, -1, -1};
+  double exit_r_const_ = 0.0;  // the constant-speed radius around the goal (TieGuard)
+  // true once minCostGlobalNode checked the band's values for near ties (or the band
+  // is exact / caller-built)
+  bool band_values_checked_ = true;
+  void settleBand();  // the check, and the exact replay on a near tie
   static constexpr uint64_t kReplayBudget = 1ull << 26;  // band-replay updates per exit
+  static constexpr double kTieEps = 1e-12;        // near-tie bound (relative, TieGuard)
+  static constexpr double kRegionMargin = 1e-9;   // the exit region: T <= t_closed (1 + this)
+  // the host mirror's values for PopOrder
+  struct MapT {
+    const DyMuPathPlanner* p;
+    double operator()(uint64_t k) const { return p->T(k); }
+  };
   // band_cells_ into the reference's insertion order, if still in grid order
   void orderBand();
   bool safeNode(unsigned i, unsigned j) const;
@@ -385,8 +423,9 @@ class DyMuPathPlanner {
   uint64_t dcells_ = 0;
   // host mirror of dT_
   mutable std::vector<double> total_cost_;
-  mutable std::vector<uint8_t> blk_ok_;
+  mutable std::vector<uint8_t> blk_ok_;  // read / written with atomic builtins (T())
   mutable uint64_t blk_missing_ = 0;
+  mutable std::mutex fetch_mu_;          // T(): one block download at a time
   unsigned nbx_ = 0, nby_ = 0;
   void* registered_ = nullptr;  // total_cost_ buffer page-locked for DMA
   double closed_limit_ = 0.0;   // CLOSED iff finite T <= closed_limit_ ...

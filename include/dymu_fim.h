@@ -142,6 +142,20 @@ int dymu_count_equal(dymu_ctx* ctx, const double* dT, uint32_t nx, uint32_t ny, 
  * planner's early exit resolves the reference's order among them. */
 int dymu_find_equal(dymu_ctx* ctx, const double* dT, uint32_t nx, uint32_t ny, uint64_t ld,
                     double value, uint64_t* idx, uint64_t cap, uint64_t* count, void* stream);
+/* The early exit's region, for the planner's near-tie guard and its exact host
+ * replay: the bounding box of the cells with T <= thr (i0, j0, i1, j1
+ * inclusive; i0 > i1 when there is none), the number of cells with lo <= T <= hi (the
+ * engine's near ties with the exit value), and r_const, the Euclidean distance from
+ * the goal (goal_i, goal_j) to the nearest cell whose speed differs from the goal's
+ * (+inf: constant speed everywhere).  Synchronises `stream`. */
+typedef struct dymu_region {
+  uint32_t i0, j0, i1, j1;
+  uint64_t n_range;
+  double r_const;
+} dymu_region;
+int dymu_region_stats(dymu_ctx* ctx, const double* dF, const double* dT, uint32_t nx, uint32_t ny,
+                      uint64_t ld, uint32_t goal_i, uint32_t goal_j, double thr, double lo,
+                      double hi, dymu_region* out, void* stream);
 /* dT[(idx[k] / nx) * ld + idx[k] % nx] = vals[k] for k < n (idx, vals: host). */
 int dymu_scatter(dymu_ctx* ctx, double* dT, uint32_t nx, uint64_t ld, const uint64_t* idx,
                  const double* vals, uint64_t n, void* stream);

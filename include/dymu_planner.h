@@ -82,6 +82,10 @@ int dymu_planner_last_stats(dymu_planner* p, dymu_stats* out);
  * out[4] reference updates the band replay evaluated, out[5] 1 if every band value
  * is the reference's (0: the replay hit its work bound) */
 int dymu_planner_last_early_exit(dymu_planner* p, double out[6]);
+/* the same, n values of: tied, open_at_limit, exact_replay, resolve_ms, replay_updates,
+ * band_exact, near_ties (comparisons of engine values rounding could flip: any sends
+ * the exit to the exact host replay), replay_threads (round 6) */
+int dymu_planner_last_early_exit_ex(dymu_planner* p, double* out, uint32_t n);
 /* how the last solve ran: 0 cold, 1 windowed re-propagation from the window
  * where the speed changed (dymu_resolve_window), 2 previous map reused */
 int dymu_planner_last_solve_kind(dymu_planner* p);
@@ -99,6 +103,9 @@ int dymu_planner_get_global_node(dymu_planner* p, uint32_t i, uint32_t j, dymu_g
 int dymu_planner_is_safe_node(dymu_planner* p, uint32_t i, uint32_t j);          /* :410-422 */
 int dymu_planner_is_fully_closed_node(dymu_planner* p, uint32_t i, uint32_t j);  /* :424-436 */
 int dymu_planner_reset_total_cost_map(dymu_planner* p);                          /* :473-485 */
+/* every node's state in bulk (ny*nx bytes, row-major: 1 CLOSED, 0 OPEN), as
+ * dymu_planner_get_global_node reports it one node at a time */
+int dymu_planner_get_node_states(dymu_planner* p, uint8_t* out);
 /* global_narrowband (:445) as the last computeTotalCostMap left it: the band
  * size; up to max (i, j) pairs written to ij in the reference's insertion order */
 int64_t dymu_planner_global_narrowband(dymu_planner* p, uint32_t* ij, int64_t max);

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -91,6 +92,7 @@ struct dymu_ctx {
   void* h_xfer = nullptr;       // host address
   void* d_xfer = nullptr;       // its device address
   uint64_t xfer_cap = 0;        // bytes
+  unsigned long long* d_region = nullptr;  // dymu_region_stats' 8 device words
   unsigned long long* d_scratch = nullptr;  // 8 words of per-call device scalars
   double* d_lut = nullptr;      // computeCostMap LUT (device copy)
   size_t lut_cap = 0;
@@ -1229,6 +1231,7 @@ int dymu_destroy(dymu_ctx* c) {
   if (c->h_mail) (void)hipHostFree(c->h_mail);
   if (c->d_band) (void)hipFree(c->d_band);
   if (c->h_xfer) (void)hipHostFree(c->h_xfer);
+  if (c->d_region) (void)hipFree(c->d_region);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return DYMU_OK;
@@ -1327,6 +1330,47 @@ int dymu_find_equal(dymu_ctx* c, const double* dT, uint32_t nx, uint32_t ny, uin
   *count = c->h_probe[0];
   const uint64_t m = std::min<uint64_t>(*count, cap);
   if (m) std::memcpy(idx, c->h_xfer, sizeof(uint64_t) * m);
+  return DYMU_OK;
+}
+
+int dymu_region_stats(dymu_ctx* c, const double* dF, const double* dT, uint32_t nx, uint32_t ny,
+                      uint64_t ld, uint32_t gi, uint32_t gj, double thr, double lo, double hi,
+                      dymu_region* out, void* stream) {
+  if (!c || !dF || !dT || !out || nx == 0 || ny == 0 || ld < nx || gi >= nx || gj >= ny)
+    return DYMU_ERR_ARG;
+  HIPC(c, hipSetDevice(c->device));
+  hipStream_t st = pick_stream(c, stream);
+  HIPC(c, hipStreamSynchronize(st));  // no earlier kernel still uses the transfer buffer
+  int rc = ensure_xfer(c, sizeof(unsigned long long) * 8);
+  if (rc) return rc;
+  if (!c->d_region) HIPC(c, hipMalloc(&c->d_region, sizeof(unsigned long long) * 8));
+  // atomics on device words (initialised by memsets), read back into pinned memory
+  unsigned long long* d = c->d_region;
+  auto* h = static_cast<unsigned long long*>(c->h_xfer);
+  HIPC(c, hipMemsetAsync(d, 0xFF, 2 * sizeof(unsigned long long), st));  // min i, min j
+  HIPC(c, hipMemsetAsync(d + 2, 0, 3 * sizeof(unsigned long long), st));  // max i, max j, count
+  HIPC(c, hipMemsetAsync(d + 5, 0xFF, sizeof(unsigned long long), st));   // min distance^2
+  double f0 = 0.0;  // the goal's speed
+  HIPC(c, hipMemcpyAsync(h + 7, dF + (uint64_t)gj * ld + gi, sizeof(double), hipMemcpyDeviceToHost,
+                         st));
+  HIPC(c, launch_region_box(dT, (int64_t)ld, nx, ny, thr, lo, hi, d, st));
+  HIPC(c, hipStreamSynchronize(st));
+  std::memcpy(&f0, &h[7], sizeof f0);
+  HIPC(c, launch_const_radius(dF, (int64_t)ld, nx, ny, gi, gj, f0, d + 5, st));
+  HIPC(c, hipMemcpyAsync(h, d, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  HIPC(c, hipStreamSynchronize(st));
+  std::memset(out, 0, sizeof *out);
+  out->n_range = h[4];
+  out->r_const = h[5] == ~0ull ? __builtin_inf() : std::sqrt((double)h[5]);
+  if (h[0] > h[2]) {  // no cell at or below thr
+    out->i0 = 1;
+    out->i1 = 0;
+    return DYMU_OK;
+  }
+  out->i0 = (uint32_t)h[0];
+  out->j0 = (uint32_t)h[1];
+  out->i1 = (uint32_t)h[2];
+  out->j1 = (uint32_t)h[3];
   return DYMU_OK;
 }
 

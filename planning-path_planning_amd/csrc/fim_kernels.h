@@ -284,6 +284,15 @@ hipError_t launch_probe(const double* T, int64_t ld, const ProbeCells& cells,
 hipError_t launch_early_mask(const double* F, double* T, int64_t ld, uint32_t nx, uint32_t ny,
                              double t_closed, uint64_t* band, unsigned long long* n_band,
                              uint64_t cap, hipStream_t st);
+// the early exit's region: bbox of the cells with T <= thr into out[0..3] (atomic
+// min i, min j, max i, max j: initialise to ~0, ~0, 0, 0) and the count of cells with
+// lo <= T <= hi added to out[4]
+hipError_t launch_region_box(const double* T, int64_t ld, uint32_t nx, uint32_t ny, double thr,
+                             double lo, double hi, unsigned long long* out, hipStream_t st);
+// least squared distance from (gi, gj) to a cell of speed != f0 into *out (atomic min:
+// initialise to ~0)
+hipError_t launch_const_radius(const double* F, int64_t ld, uint32_t nx, uint32_t ny, uint32_t gi,
+                               uint32_t gj, double f0, unsigned long long* out, hipStream_t st);
 // *p = v, in stream order (no host-to-device copy for a per-call scalar)
 hipError_t launch_store_u64(unsigned long long* p, unsigned long long v, hipStream_t st);
 // T[(idx / nx) * ld + idx % nx] = vals[k]

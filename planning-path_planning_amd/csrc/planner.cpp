@@ -11,6 +11,7 @@
 //     on first read (path extraction reads a narrow band around the path) or
 //     all of it for the matrix getters.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -116,6 +117,7 @@ bool DyMuPathPlanner::initGlobalLayer(double globalres, double localres, unsigne
   closed_limit_ = 0.0;
   band_cells_.clear();
   band_unordered_ = false;
+  band_values_checked_ = true;
   open_at_limit_.clear();
   node_state_.clear();
   propagated_extra_.clear();
@@ -160,21 +162,16 @@ unsigned host_threads() {
   return h ? std::min(h, 64u) : 1u;
 }
 
-// body(j0, j1) over row ranges of [0, ny) on up to host_threads() threads (at
-// least 64 rows each).  Every loop run this way writes only the node it visits
-// and reads fields no iteration of the same loop writes, so the split changes no
-// value -- the results are those of the reference's single raster loop.
-// Exceptions thrown by body on a worker thread are carried back and rethrown on
-// the calling thread (a throw escaping a std::thread would std::terminate); the
-// started threads are joined on every path, a failed thread start included.
+// body(t) for t in [0, nt) on nt threads (the caller's among them).  Exceptions
+// thrown by body on a worker thread are carried back and rethrown on the calling
+// thread (a throw escaping a std::thread would std::terminate); the started threads
+// are joined on every path, a failed thread start included.
 template <class Body>
-void parallel_rows(unsigned ny, Body&& body) {
-  const unsigned nt = std::max(1u, std::min(host_threads(), ny / 64));
-  if (nt == 1) {
-    body(0u, ny);
+void parallel_tasks(unsigned nt, Body&& body) {
+  if (nt <= 1) {
+    body(0u);
     return;
   }
-  const unsigned step = (ny + nt - 1) / nt;
   std::vector<std::exception_ptr> errs(nt);
   struct Joiner {
     std::vector<std::thread> pool;
@@ -184,28 +181,39 @@ void parallel_rows(unsigned ny, Body&& body) {
     }
   } J;
   J.pool.reserve(nt - 1);
-  auto run = [&body, &errs](unsigned t, unsigned j0, unsigned j1) {
+  auto run = [&body, &errs](unsigned t) {
     try {
-      body(j0, j1);
+      body(t);
     } catch (...) {
       errs[t] = std::current_exception();
     }
   };
   try {
-    for (unsigned t = 1; t < nt; ++t) {
-      const unsigned j0 = t * step, j1 = std::min(ny, j0 + step);
-      if (j0 < j1) J.pool.emplace_back(run, t, j0, j1);
-    }
+    for (unsigned t = 1; t < nt; ++t) J.pool.emplace_back(run, t);
   } catch (...) {  // std::system_error from a thread start: finish what started, rethrow
     for (auto& th : J.pool) th.join();
     J.pool.clear();
     throw;
   }
-  run(0u, 0u, std::min(ny, step));
+  run(0u);
   for (auto& th : J.pool) th.join();
   J.pool.clear();
   for (auto& e : errs)
     if (e) std::rethrow_exception(e);
+}
+
+// body(j0, j1) over row ranges of [0, ny) on up to host_threads() threads (at
+// least 64 rows each).  Every loop run this way writes only the node it visits
+// and reads fields no iteration of the same loop writes, so the split changes no
+// value -- the results are those of the reference's single raster loop.
+template <class Body>
+void parallel_rows(unsigned ny, Body&& body) {
+  const unsigned nt = std::max(1u, std::min(host_threads(), ny / 64));
+  const unsigned step = (ny + nt - 1) / nt;
+  parallel_tasks(nt, [&](unsigned t) {
+    const unsigned j0 = t * step, j1 = std::min(ny, j0 + step);
+    if (t == 0 || j0 < j1) body(j0, j1);
+  });
 }
 
 }  // namespace
@@ -547,20 +555,25 @@ bool DyMuPathPlanner::syncSpeed(unsigned& i0, unsigned& i1, unsigned& j0, unsign
   return true;
 }
 
+// Thread-safe (the band replay's threads read through it): a block's flag is read
+// with acquire and set with release after its download, downloads one at a time.
 double DyMuPathPlanner::T(uint64_t k) const {
-  if (blk_missing_) {
+  if (__atomic_load_n(&blk_missing_, __ATOMIC_ACQUIRE)) {
     const unsigned j = (unsigned)(k / nx_), i = (unsigned)(k % nx_);
     const uint64_t b = (uint64_t)(j / kBlk) * nbx_ + i / kBlk;
-    if (!blk_ok_[b]) {
-      const unsigned bi = (i / kBlk) * kBlk, bj = (j / kBlk) * kBlk;
-      const unsigned w = std::min(kBlk, nx_ - bi), h = std::min(kBlk, ny_ - bj);
-      const uint64_t o = idx(bi, bj);
-      if (dymu_memcpy2d_d2h(ctx_, &total_cost_[o], sizeof(double) * nx_, dT_ + o,
-                            sizeof(double) * nx_, sizeof(double) * w, h) != DYMU_OK)
-        throw std::runtime_error(std::string("dymu: total-cost download failed: ") +
-                                 dymu_last_error(ctx_));
-      blk_ok_[b] = 1;
-      --blk_missing_;
+    if (!__atomic_load_n(&blk_ok_[b], __ATOMIC_ACQUIRE)) {
+      std::lock_guard<std::mutex> lock(fetch_mu_);
+      if (!__atomic_load_n(&blk_ok_[b], __ATOMIC_RELAXED)) {
+        const unsigned bi = (i / kBlk) * kBlk, bj = (j / kBlk) * kBlk;
+        const unsigned w = std::min(kBlk, nx_ - bi), h = std::min(kBlk, ny_ - bj);
+        const uint64_t o = idx(bi, bj);
+        if (dymu_memcpy2d_d2h(ctx_, &total_cost_[o], sizeof(double) * nx_, dT_ + o,
+                              sizeof(double) * nx_, sizeof(double) * w, h) != DYMU_OK)
+          throw std::runtime_error(std::string("dymu: total-cost download failed: ") +
+                                   dymu_last_error(ctx_));
+        __atomic_store_n(&blk_ok_[b], (uint8_t)1, __ATOMIC_RELEASE);
+        __atomic_sub_fetch(&blk_missing_, 1, __ATOMIC_RELEASE);
+      }
     }
   }
   return total_cost_[k];
@@ -698,6 +711,7 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
   blk_missing_ = blk_ok_.size();
   band_cells_.clear();
   band_unordered_ = false;
+  band_values_checked_ = true;
   open_at_limit_.clear();
   node_state_.clear();
   propagated_extra_.clear();
@@ -714,6 +728,33 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
   // tentative values; every other cell +inf.  dT_ is no longer a converged map.
   solved_ = false;
   closed_limit_ = t_closed;
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint64_t g = idx(goal_i_, goal_j_), s = idx(si, sj);
+  // The region the exit is decided on: the cells of T <= t_closed (a margin far above
+  // the engine's error) and their band, one cell around; and the near-tie guard over it
+  // (pop_order.hpp): the engine's values order cells as the reference's do only where
+  // no rounding can flip the order
+  dymu_region reg{};
+  reg.i0 = 1;
+  reg.i1 = 0;
+  const double thr = t_closed < kInf ? t_closed * (1 + kRegionMargin) : kInf;
+  if (dymu_region_stats(ctx_, dF_, dT_, nx_, ny_, nx_, goal_i_, goal_j_, thr,
+                        t_closed * (1 - kTieEps), t_closed * (1 + kTieEps), &reg,
+                        nullptr) != DYMU_OK)
+    throw std::runtime_error(std::string("dymu_region_stats failed: ") + dymu_last_error(ctx_));
+  int64_t box[4] = {0, 0, -1, -1};  // inclusive; empty when nothing was reached
+  if (reg.i0 <= reg.i1) {
+    box[0] = reg.i0 > 0 ? reg.i0 - 1 : 0;
+    box[1] = reg.j0 > 0 ? reg.j0 - 1 : 0;
+    box[2] = std::min<int64_t>((int64_t)reg.i1 + 1, nx_ - 1);
+    box[3] = std::min<int64_t>((int64_t)reg.j1 + 1, ny_ - 1);
+  }
+  TieGuard guard(nx_, goal_i_, goal_j_, speed_[g], reg.r_const);
+  have_start_ = true;  // for insertionOrder's / minCostGlobalNode's exact fallback
+  exit_r_const_ = reg.r_const;
+  start_i_ = si;
+  start_j_ = sj;
+  std::copy(box, box + 4, exit_box_);
   std::vector<uint64_t> band(std::max<uint64_t>(4096, 4 * (uint64_t)(nx_ + ny_)));
   uint64_t nb = 0;
   for (;;) {
@@ -727,13 +768,18 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
   }
   band.resize(nb);
   std::sort(band.begin(), band.end());
-  const auto t0 = std::chrono::steady_clock::now();
-  const uint64_t g = idx(goal_i_, goal_j_), s = idx(si, sj);
-  auto mirror = [this](uint64_t k) { return T(k); };
-  PopOrder<decltype(mirror)> po(mirror, nx_, ny_, g);
+  PopOrder<MapT> po(MapT{this}, nx_, ny_, g, &guard);
+  // the exit moment: the last of the start and its nb4 the reference pops (all five
+  // CLOSED; the latest has the largest value, t_closed)
+  const uint64_t probes[5] = {s, s - nx_, s - 1, s + 1, s + nx_};
+  uint64_t last = s;
+  for (int q = 1; q < 5; ++q)
+    if (po.popBefore(last, probes[q])) last = probes[q];
   // Cells of exactly t_closed: the reference pops them in insertion order and stops
-  // right after the last of the start and its nb4, so those it pops later stay in
-  // the band (with their value).  Resolve which, from the values (pop_order.hpp).
+  // right after `last`, so those it pops later stay in the band (with their value).
+  // Resolve which, from the values (pop_order.hpp).  An engine tie with the exit value
+  // is the reference's only as a mirror image of a probe of that value; a cell the
+  // engine puts within eps of it, but not on it, is a near tie.
   if (t_closed < kInf) {
     std::vector<uint64_t> eq(256);
     uint64_t n_eq = 0;
@@ -746,30 +792,28 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
     }
     eq.resize(n_eq);
     early_info_.tied = n_eq;
-    if (n_eq > 1) {
-      const uint64_t probes[5] = {s, s - nx_, s - 1, s + 1, s + nx_};
-      uint64_t last = s;
-      bool have = false;
+    for (const uint64_t x : eq) {
+      bool trusted = false;
       for (const uint64_t q : probes)
-        if (T(q) == t_closed && (!have || po.popBefore(last, q))) {
-          last = q;
-          have = true;
-        }
+        trusted = trusted || (T(q) == t_closed && (q == x || guard.mirror(x, q)));
+      if (!trusted) ++guard.near;
+    }
+    guard.near += reg.n_range > n_eq ? reg.n_range - n_eq : 0;
+    if (n_eq > 1) {
       for (const uint64_t x : eq)
         if (x != last && po.popBefore(last, x)) open_at_limit_.push_back(x);
       std::sort(open_at_limit_.begin(), open_at_limit_.end());
-      // an undetermined order (pop_order.hpp) leaves every tied cell CLOSED, as the
-      // engine's state has it; the exact host replay below takes over where it may
-      if (po.degenerate()) open_at_limit_.clear();
     }
   }
   const double ms_order =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  // an undetermined or near-tied order: the exact host replay decides the exit
+  bool exact = po.degenerate() || guard.near > 0;
   // the band with the cells the reference left OPEN at t_closed: they join it, and
   // a neighbour of theirs stays in it only if it has another CLOSED neighbour
   // (otherwise it was never reached: +inf)
   std::vector<uint64_t> unreached;
-  if (!open_at_limit_.empty()) {
+  if (!exact && !open_at_limit_.empty()) {
     std::vector<uint64_t> add(open_at_limit_);
     for (const uint64_t x : open_at_limit_) {
       const unsigned i = (unsigned)(x % nx_), j = (unsigned)(x / nx_);
@@ -797,58 +841,61 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
     std::sort(kept.begin(), kept.end());
     band.swap(kept);
     nb = band.size();
-    if (!unreached.empty()) {
-      const std::vector<double> inf(unreached.size(), kInf);
-      if (dymu_scatter(ctx_, dT_, nx_, nx_, unreached.data(), inf.data(), unreached.size(),
-                       nullptr) != DYMU_OK)
-        throw std::runtime_error(std::string("dymu_scatter failed: ") + dymu_last_error(ctx_));
-      for (const uint64_t y : unreached) {
-        (void)T(y);
-        total_cost_[y] = kInf;
-      }
+  }
+  std::vector<double> vals;
+  if (nb && !exact) {
+    exact = replayBand(last, band, vals, guard);
+  }
+  early_info_.near_ties = guard.near;
+  early_info_.open_at_limit = open_at_limit_.size();
+  if (exact) {
+    // the reference replayed exactly on the host over the region (no size limit)
+    early_info_.exact_replay = 1;
+    if (std::getenv("DYMU_ORDER_DEBUG"))
+      std::fprintf(stderr,
+                   "[dymu] exact exit: near ties %llu (first (%llu,%llu) %.17g vs (%llu,%llu) "
+                   "%.17g; mirror below %.17g), degenerate %d (reason %d)\n",
+                   (unsigned long long)guard.near, (unsigned long long)(guard.first[0] % nx_),
+                   (unsigned long long)(guard.first[0] / nx_), guard.first_t[0],
+                   (unsigned long long)(guard.first[1] % nx_),
+                   (unsigned long long)(guard.first[1] / nx_), guard.first_t[1],
+                   guard.trust_below, (int)po.degenerate(), po.why());
+    const bool r = exactEarlyExit(si, sj, box);
+    early_info_.resolve_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return r;
+  }
+  if (!unreached.empty()) {
+    const std::vector<double> inf(unreached.size(), kInf);
+    if (dymu_scatter(ctx_, dT_, nx_, nx_, unreached.data(), inf.data(), unreached.size(),
+                     nullptr) != DYMU_OK)
+      throw std::runtime_error(std::string("dymu_scatter failed: ") + dymu_last_error(ctx_));
+    for (const uint64_t y : unreached) {
+      (void)T(y);
+      total_cost_[y] = kInf;
     }
   }
-  early_info_.open_at_limit = open_at_limit_.size();
-  bool degenerate = po.degenerate();
-  if (degenerate && std::getenv("DYMU_ORDER_DEBUG"))
-    std::fprintf(stderr, "[dymu] exit order undetermined: reason %d at cell %llu\n", po.why(),
-                 (unsigned long long)po.whyCell());
-  if (nb && !degenerate) {
-    std::vector<double> vals;
-    uint64_t last = s;
-    for (const uint64_t q : {s - nx_, s - 1, s + 1, s + nx_})
-      if (closedCell(q) && po.popBefore(last, q)) last = q;
-    degenerate = replayBand(last, band, vals);
-    if (!degenerate) {
-      rc = dymu_scatter(ctx_, dT_, nx_, nx_, band.data(), vals.data(), nb, nullptr);
-      if (rc != DYMU_OK)
-        throw std::runtime_error(std::string("dymu_scatter failed: ") + dymu_last_error(ctx_));
-      // blocks fetched during the replay hold the pre-replay band values
-      for (uint64_t q = 0; q < nb; ++q) total_cost_[band[q]] = vals[q];
+  if (nb) {
+    rc = dymu_scatter(ctx_, dT_, nx_, nx_, band.data(), vals.data(), nb, nullptr);
+    if (rc != DYMU_OK)
+      throw std::runtime_error(std::string("dymu_scatter failed: ") + dymu_last_error(ctx_));
+    // blocks fetched during the replay hold the pre-replay band values
+    for (uint64_t q = 0; q < nb; ++q) {
+      (void)T(band[q]);
+      total_cost_[band[q]] = vals[q];
     }
   }
   early_info_.resolve_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  if (degenerate) {
-    // a node whose least neighbour has its own value (speeds below the rounding of
-    // the total cost): the values do not determine the reference's order.  Replay
-    // the reference exactly on the host, up to kExactReplayCells; beyond that keep
-    // the engine's state (every cell of exactly t_closed CLOSED) and say so.
-    if ((uint64_t)nx_ * ny_ <= kExactReplayCells) {
-      early_info_.exact_replay = 1;
-      return exactEarlyExit(si, sj);
-    }
-    log_warn("computeTotalCostMap: degenerate ties at the exit value; the pop order among "
-             "them is not reproduced (grid larger than the exact-replay limit)");
-  }
   if (std::getenv("DYMU_ORDER_DEBUG"))
-    std::fprintf(stderr, "[dymu] early exit: t_closed %.17g band %llu tied %llu open %llu "
-                 "degenerate %d, %.1f ms order + %.1f ms band\n", t_closed,
+    std::fprintf(stderr, "[dymu] early exit: t_closed %.17g band %llu tied %llu open %llu, "
+                 "%.1f ms order + %.1f ms band on %u threads\n", t_closed,
                  (unsigned long long)nb, (unsigned long long)early_info_.tied,
-                 (unsigned long long)open_at_limit_.size(), (int)degenerate, ms_order,
-                 early_info_.resolve_ms - ms_order);
+                 (unsigned long long)open_at_limit_.size(), ms_order,
+                 early_info_.resolve_ms - ms_order, early_info_.replay_threads);
   band_cells_ = std::move(band);
   band_unordered_ = band_cells_.size() > 1;
+  band_values_checked_ = false;  // minCostGlobalNode checks them for near ties first
   return nb > 0;
 }
 
@@ -864,13 +911,18 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
 // OPEN value at moment m is >= T(m) >= any CLOSED value then (the FMM invariant), so
 // an axis with a CLOSED side takes that side and the recursion only follows axes
 // whose two sides are OPEN -- cells next to the front, at strictly earlier pops (x's
-// neighbours are not adjacent to each other).  Returns true when the pop order was
-// undetermined (degenerate ties, pop_order.hpp): the values are not to be used.
+// neighbours are not adjacent to each other).
+// The band cells are independent given the CLOSED values: host threads take
+// contiguous runs of them, each with its own memo and order cache (a walk back stays
+// near its band cell, so little work is repeated across threads).  Every comparison
+// of two cells' values goes through a copy of the guard; their near ties are summed
+// into `guard`.  Returns true when the values are not to be used: the pop order was
+// undetermined or near-tied, or a replay hit its work bound -- the caller then
+// replays the reference exactly.
 bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& band,
-                                 std::vector<double>& out) {
-  auto mirror = [this](uint64_t k) { return T(k); };
-  using Order = PopOrder<decltype(mirror)>;
-  // open-addressing memo of upd(k, s), keyed k * 4 + s + 1 (0 = empty)
+                                 std::vector<double>& out, TieGuard& guard) {
+  using Order = PopOrder<MapT>;
+  // open-addressing map uint64 -> double, keys != 0
   struct Memo {
     std::vector<uint64_t> key;
     std::vector<double> v;
@@ -904,29 +956,33 @@ bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& ban
   };
   struct Replay {
     DyMuPathPlanner& pl;
+    TieGuard guard;                // this thread's copy (near ties counted here)
     Order po;
     const double* F;
     int64_t NX, NY;
     uint64_t last;                 // the exit moment
-    double lim;                    // closed_limit_
+    double lim;                    // closed_limit_ (T(last))
     const std::vector<uint64_t>& open;  // open_at_limit_
     uint64_t budget;               // upd evaluations left before giving up
-    Memo memo;                     // upd(k, s)
-    std::unordered_map<uint64_t, double> bmemo;  // band values at the exit
+    Memo memo;                     // upd(k, s), keyed k * 4 + s + 1
+    Memo bmemo;                    // band values at the exit, keyed k + 1
     uint64_t band_k = ~0ull;       // the band cell being evaluated at the exit
     bool overrun = false;          // the budget or the depth bound was hit
 
-    bool in_grid(int64_t i, int64_t j) const { return i >= 0 && j >= 0 && i < NX && j < NY; }
-    double tv(int64_t i, int64_t j) const {  // T(i, j), fetching its block on first use
-      const uint64_t b = (uint64_t)(j / kBlk) * pl.nbx_ + (uint64_t)(i / kBlk);
-      const uint64_t k = (uint64_t)(j * NX + i);
-      if (pl.blk_missing_ && !pl.blk_ok_[b]) return pl.T(k);
-      return pl.total_cost_[k];
+    Replay(DyMuPathPlanner& p, const TieGuard& g, uint64_t gl, uint64_t lst, uint64_t b)
+        : pl(p), guard(g), po(MapT{&p}, p.nx_, p.ny_, gl, &guard),
+          F(p.speed_.data()), NX(p.nx_), NY(p.ny_), last(lst), lim(p.closed_limit_),
+          open(p.open_at_limit_), budget(b) {
+      guard.near = 0;
     }
+    bool in_grid(int64_t i, int64_t j) const { return i >= 0 && j >= 0 && i < NX && j < NY; }
+    double tv(int64_t i, int64_t j) const { return pl.T((uint64_t)(j * NX + i)); }
     // closedCell with T already loaded (node_state_ is empty here: propagate cleared it)
-    bool closed(uint64_t k, double t) const {
-      if (!(t < kInf) || t > lim) return false;
-      return t < lim || open.empty() || !std::binary_search(open.begin(), open.end(), k);
+    bool closed(uint64_t k, double t) {
+      if (!(t < kInf)) return false;
+      const int c = guard.cmp(k, t, last, lim);
+      if (c != 0) return c < 0;
+      return open.empty() || !std::binary_search(open.begin(), open.end(), k);
     }
     // value of (i, j) if it is CLOSED by moment c (value tc), else +inf
     double closed_by(int64_t i, int64_t j, uint64_t c, double tc) {
@@ -934,8 +990,9 @@ bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& ban
       const uint64_t k = (uint64_t)(j * NX + i);
       const double t = tv(i, j);
       if (!closed(k, t)) return kInf;
-      if (t < tc || k == c) return t;
-      if (t > tc) return kInf;
+      if (k == c) return t;
+      const int r = guard.cmp(k, t, c, tc);
+      if (r != 0) return r < 0 ? t : kInf;
       return po.popBefore(k, c) ? t : kInf;
     }
     // the reference update (:504-535), -ffp-contract=off
@@ -985,13 +1042,12 @@ bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& ban
     // a band cell's value at the exit, memoised
     double bandval(int64_t i, int64_t j, int depth) {
       const uint64_t k = (uint64_t)(j * NX + i);
-      auto it = bmemo.find(k);
-      if (it != bmemo.end()) return it->second;
+      if (const double* hit = bmemo.find(k + 1)) return *hit;
       const uint64_t saved = band_k;
       band_k = k;
-      const double v = val(i, j, last, tv(last % NX, last / NX), depth + 1);
+      const double v = val(i, j, last, lim, depth + 1);
       band_k = saved;
-      bmemo.emplace(k, v);
+      bmemo.put(k + 1, v);
       return v;
     }
     // the reference update of k at the pop of its neighbour in nb4 slot s (:462-465)
@@ -999,7 +1055,7 @@ bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& ban
       const uint64_t k = (uint64_t)(j * NX + i);
       const uint64_t key = k * 4 + (uint64_t)s + 1;
       if (const double* hit = memo.find(key)) return *hit;
-      if (depth > 3000 || budget == 0) {  // give up (~1 MB of stack): the engine's value, flagged
+      if (depth > 3000 || budget == 0) {  // give up (~1 MB of stack)
         overrun = true;
         return tv(i, j);
       }
@@ -1015,126 +1071,334 @@ bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& ban
       memo.put(key, v);
       return v;
     }
-  } rec{*this, Order(mirror, nx_, ny_, idx(goal_i_, goal_j_)), speed_.data(), (int64_t)nx_,
-        (int64_t)ny_, last, closed_limit_, open_at_limit_, kReplayBudget, {}, {}};
-  out.resize(band.size());
-  for (size_t q = 0; q < band.size(); ++q)
-    out[q] = rec.bandval((int64_t)(band[q] % nx_), (int64_t)(band[q] / nx_), 0);
-  early_info_.replay_updates = kReplayBudget - rec.budget;
-  early_info_.band_exact = rec.overrun ? 0 : 1;
-  if (rec.overrun)
-    log_warn("computeTotalCostMap: the band replay hit its work bound; some band values are "
-             "the engine's (DESIGN.md s3)");
-  if (rec.po.degenerate() && std::getenv("DYMU_ORDER_DEBUG")) {
-    const uint64_t k = rec.po.whyCell();
-    std::fprintf(stderr, "[dymu] order undetermined: reason %d at (%llu, %llu) T=%.17g\n",
-                 rec.po.why(), (unsigned long long)(k % nx_), (unsigned long long)(k / nx_), T(k));
+  };
+  const uint64_t g = idx(goal_i_, goal_j_);
+  out.assign(band.size(), kInf);
+  // threads: at least 64 band cells each; the work bound is shared out per thread
+  const unsigned nt = std::max(1u, std::min(host_threads(), (unsigned)std::min<uint64_t>(
+                                                                 band.size() / 64, 1u << 16)));
+  std::vector<uint64_t> used(nt, 0);
+  std::vector<TieGuard> tg(nt, guard);  // each thread's guard at its end
+  std::vector<uint8_t> bad(nt, 0);
+  // runs of band cells taken from a shared counter: the work per cell varies by orders
+  // of magnitude along the front (where a staircase front walks far back), so static
+  // shares leave most threads idle; a thread keeps its memo across its runs
+  const uint64_t run = std::max<uint64_t>(16, band.size() / ((uint64_t)nt * 16));
+  std::atomic<uint64_t> next_run{0};
+  std::vector<double> tms(nt, 0.0);
+  const auto tp0 = std::chrono::steady_clock::now();
+  parallel_tasks(nt, [&](unsigned t) {
+    const auto tt0 = std::chrono::steady_clock::now();
+    struct Stamp {
+      double& ms;
+      std::chrono::steady_clock::time_point t0;
+      ~Stamp() {
+        ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      }
+    } stamp{tms[t], tt0};
+    Replay rec(*this, guard, g, last, kReplayBudget / nt);
+    for (;;) {
+      const uint64_t q0 = next_run.fetch_add(run, std::memory_order_relaxed);
+      if (q0 >= band.size() || rec.overrun || rec.po.degenerate()) break;
+      const uint64_t q1 = std::min<uint64_t>(band.size(), q0 + run);
+      for (uint64_t q = q0; q < q1 && !rec.overrun && !rec.po.degenerate(); ++q)
+        out[q] = rec.bandval((int64_t)(band[q] % nx_), (int64_t)(band[q] / nx_), 0);
+    }
+    used[t] = kReplayBudget / nt - rec.budget;
+    tg[t] = rec.guard;
+    bad[t] = rec.overrun || rec.po.degenerate();
+    if (rec.po.degenerate() && std::getenv("DYMU_ORDER_DEBUG")) {
+      const uint64_t k = rec.po.whyCell();
+      std::fprintf(stderr, "[dymu] order undetermined: reason %d at (%llu, %llu)\n",
+                   rec.po.why(), (unsigned long long)(k % nx_), (unsigned long long)(k / nx_));
+    }
+  });
+  if (std::getenv("DYMU_ORDER_DEBUG")) {
+    std::fprintf(stderr, "[dymu] band replay %.1f ms, per thread:",
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0)
+                     .count());
+    for (unsigned t = 0; t < nt; ++t) std::fprintf(stderr, " %.1f/%llu", tms[t], (unsigned long long)used[t]);
+    std::fprintf(stderr, "\n");
   }
-  return rec.po.degenerate();
+  early_info_.replay_threads = nt;
+  early_info_.replay_updates = 0;
+  bool give_up = false;
+  for (unsigned t = 0; t < nt; ++t) {
+    early_info_.replay_updates += used[t];
+    if (!guard.near && tg[t].near) {
+      std::copy(tg[t].first, tg[t].first + 2, guard.first);
+      std::copy(tg[t].first_t, tg[t].first_t + 2, guard.first_t);
+    }
+    guard.near += tg[t].near;
+    give_up = give_up || bad[t];
+  }
+  return give_up || guard.near > 0;
 }
 
 // band_cells_ after a GPU early exit are in grid order: put them in the reference's
-// insertion order (pop_order.hpp) before anyone reads the order
+// insertion order (pop_order.hpp) before anyone reads the order.  (The exit has
+// already checked the order for near ties: the exact replay ran otherwise.)
 void DyMuPathPlanner::orderBand() {
   if (!band_unordered_) return;
   band_unordered_ = false;
-  auto mirror = [this](uint64_t k) { return T(k); };
-  PopOrder<decltype(mirror)> po(mirror, nx_, ny_, idx(goal_i_, goal_j_));
+  PopOrder<MapT> po(MapT{this}, nx_, ny_, idx(goal_i_, goal_j_));
   std::vector<uint64_t> b(band_cells_);
   std::stable_sort(b.begin(), b.end(),
                    [&po](uint64_t x, uint64_t y) { return po.insBefore(x, y); });
   if (!po.degenerate()) band_cells_.swap(b);  // else keep grid order
 }
 
-// computeTotalCostMap (:364-408) replayed exactly on the host: the reference FMM with
-// its band as a heap keyed (T, first-insertion sequence) -- the pops of the
-// first-strict-minimum scan (:551-568) in the same order -- until the start and its
-// nb4 are CLOSED.  Used when the GPU's early exit met equal total costs whose order
-// decides the CLOSED set or a band value (constant-speed maps: every distance ties):
-// O(m log m) for the m cells the reference reaches.  The map, the node states, the
-// band (insertion order) and global_propagated_nodes become the reference's.
-bool DyMuPathPlanner::exactEarlyExit(unsigned si, unsigned sj) {
-  const uint64_t n = (uint64_t)nx_ * ny_;
+// The reference FMM replayed exactly on the host: its band as a heap keyed (T,
+// first-insertion sequence) -- the pops of the first-strict-minimum scan (:551-568) in
+// the same order -- from the goal until the start (si, sj) and its nb4 are CLOSED
+// (computeTotalCostMap :364-408; si < 0: until the band empties, :443-468).  It runs
+// over a box (inclusive; empty: the whole grid): every cell the reference pops at the
+// exit has a value at most t_closed, and the caller's box holds every cell the engine
+// puts below t_closed (1 + kRegionMargin) plus a ring; a pop whose neighbour lies
+// outside it means the box was short, and the replay restarts on the whole grid.
+// O(m log m) for the m cells the reference reaches.
+DyMuPathPlanner::HostFmm DyMuPathPlanner::hostFmm(int64_t si, int64_t sj,
+                                                  const int64_t box_in[4]) const {
   const double* F = speed_.data();
-  std::vector<double> T(n, kInf);
-  std::vector<uint8_t> closed(n, 0);
-  std::vector<uint64_t> order;  // cells in the order they first became finite
-  struct E {
-    double t;
-    uint64_t seq, k;
-  };
-  auto later = [](const E& a, const E& b) { return a.t > b.t || (a.t == b.t && a.seq > b.seq); };
-  std::vector<E> heap;
-  std::vector<uint64_t> first(n, 0);
-  std::vector<uint8_t> in_band(n, 0);
-  const uint64_t g = idx(goal_i_, goal_j_), s = idx(si, sj);
-  T[g] = 0.0;
-  first[g] = 0;
-  order.push_back(g);
-  in_band[g] = 1;
-  heap.push_back({0.0, 0, g});
-  uint64_t band = 1;
-  auto fully_closed = [&] {  // :424-436 (the start is interior: safeNode)
-    return closed[s] && closed[s - nx_] && closed[s - 1] && closed[s + 1] && closed[s + nx_];
-  };
-  while (band > 0 && !fully_closed()) {
-    std::pop_heap(heap.begin(), heap.end(), later);
-    const E e = heap.back();
-    heap.pop_back();
-    if (!in_band[e.k] || e.t != T[e.k]) continue;  // a superseded entry
-    in_band[e.k] = 0;
-    --band;
-    closed[e.k] = 1;
-    const unsigned i = (unsigned)(e.k % nx_), j = (unsigned)(e.k / nx_);
-    const int64_t nb[4][2] = {{i, (int64_t)j - 1}, {(int64_t)i - 1, j}, {i + 1, j}, {i, j + 1}};
-    for (const auto& q : nb) {
-      if (q[0] < 0 || q[1] < 0 || q[0] >= nx_ || q[1] >= ny_) continue;
-      const uint64_t k = idx((unsigned)q[0], (unsigned)q[1]);
-      if (closed[k] || !(F[k] < kInf)) continue;
-      // propagateGlobalNode (:500-546) from the current values
-      const unsigned a = (unsigned)q[0], b = (unsigned)q[1];
-      const double Ty = (b > 0 && b + 1 < ny_) ? std::fmin(T[k + nx_], T[k - nx_])
-                        : b == 0              ? (b + 1 < ny_ ? T[k + nx_] : kInf)
-                                              : T[k - nx_];
-      const double Tx = (a > 0 && a + 1 < nx_) ? std::fmin(T[k - 1], T[k + 1])
-                        : a == 0              ? (a + 1 < nx_ ? T[k + 1] : kInf)
-                                              : T[k - 1];
-      const double C = F[k];
-      double u;
-      if ((std::fabs(Tx - Ty) < C) && (Tx < kInf) && (Ty < kInf))
-        u = (Tx + Ty + std::sqrt(2 * (C * C) - ((Tx - Ty) * (Tx - Ty)))) / 2;
-      else
-        u = std::fmin(Tx, Ty) + C;
-      if (u < T[k]) {
-        if (T[k] == kInf) {
-          first[k] = order.size();
-          order.push_back(k);
-          in_band[k] = 1;
-          ++band;
+  HostFmm r;
+  r.bx[0] = r.bx[1] = 0;
+  r.bx[2] = (int64_t)nx_ - 1;
+  r.bx[3] = (int64_t)ny_ - 1;
+  if (box_in && box_in[0] <= box_in[2]) {  // the region grown by two more cells
+    r.bx[0] = std::max<int64_t>(0, box_in[0] - 2);
+    r.bx[1] = std::max<int64_t>(0, box_in[1] - 2);
+    r.bx[2] = std::min<int64_t>(nx_ - 1, box_in[2] + 2);
+    r.bx[3] = std::min<int64_t>(ny_ - 1, box_in[3] + 2);
+  }
+  for (;;) {
+    const int64_t* bx = r.bx;
+    const int64_t W = bx[2] - bx[0] + 1, H = bx[3] - bx[1] + 1;
+    r.W = W;
+    const uint64_t m = (uint64_t)W * (uint64_t)H;
+    r.T.assign(m, kInf);
+    r.st.assign(m, 0);  // 1 CLOSED, 2 in the band
+    r.order.clear();
+    std::vector<uint64_t> first(m, 0);
+    struct E {
+      double t;
+      uint64_t seq, k;  // k: box-local
+    };
+    auto later = [](const E& a, const E& b) { return a.t > b.t || (a.t == b.t && a.seq > b.seq); };
+    std::vector<E> heap;
+    auto loc = [&](int64_t i, int64_t j) { return (uint64_t)((j - bx[1]) * W + (i - bx[0])); };
+    auto inbox = [&](int64_t i, int64_t j) {
+      return i >= bx[0] && j >= bx[1] && i <= bx[2] && j <= bx[3];
+    };
+    const uint64_t g = loc(goal_i_, goal_j_);
+    r.T[g] = 0.0;
+    r.order.push_back(idx(goal_i_, goal_j_));
+    r.st[g] = 2;
+    heap.push_back({0.0, 0, g});
+    r.band = 1;
+    bool short_box = false;
+    const bool early = si >= 0;
+    const uint64_t sl = early ? loc(si, sj) : 0;
+    auto fully_closed = [&] {  // :424-436 (the start is interior: safeNode)
+      return early && r.st[sl] == 1 && r.st[sl - W] == 1 && r.st[sl - 1] == 1 &&
+             r.st[sl + 1] == 1 && r.st[sl + W] == 1;
+    };
+    while (r.band > 0 && !fully_closed() && !short_box) {
+      std::pop_heap(heap.begin(), heap.end(), later);
+      const E e = heap.back();
+      heap.pop_back();
+      if (r.st[e.k] != 2 || e.t != r.T[e.k]) continue;  // a superseded entry
+      r.st[e.k] = 1;
+      --r.band;
+      const int64_t i = bx[0] + (int64_t)(e.k % (uint64_t)W), j = bx[1] + (int64_t)(e.k / (uint64_t)W);
+      const int64_t nb[4][2] = {{i, j - 1}, {i - 1, j}, {i + 1, j}, {i, j + 1}};
+      for (const auto& q : nb) {
+        if (q[0] < 0 || q[1] < 0 || q[0] >= nx_ || q[1] >= ny_) continue;
+        if (!inbox(q[0], q[1])) {
+          short_box = true;  // the reference reaches beyond the box
+          break;
         }
-        T[k] = u;
-        heap.push_back({u, first[k], k});
-        std::push_heap(heap.begin(), heap.end(), later);
+        const uint64_t k = loc(q[0], q[1]);
+        const uint64_t kg = idx((unsigned)q[0], (unsigned)q[1]);
+        if (r.st[k] == 1 || !(F[kg] < kInf)) continue;
+        // propagateGlobalNode (:500-546) from the current values (a neighbour off the
+        // grid: the other one alone; off the box: +inf, never reached)
+        const int64_t a = q[0], b = q[1];
+        auto tt = [&](int64_t x, int64_t y) { return inbox(x, y) ? r.T[loc(x, y)] : kInf; };
+        const double Ty = (b > 0 && b + 1 < ny_) ? std::fmin(tt(a, b + 1), tt(a, b - 1))
+                          : b == 0              ? (b + 1 < ny_ ? tt(a, b + 1) : kInf)
+                                                : tt(a, b - 1);
+        const double Tx = (a > 0 && a + 1 < nx_) ? std::fmin(tt(a - 1, b), tt(a + 1, b))
+                          : a == 0              ? (a + 1 < nx_ ? tt(a + 1, b) : kInf)
+                                                : tt(a - 1, b);
+        const double C = F[kg];
+        double u;
+        if ((std::fabs(Tx - Ty) < C) && (Tx < kInf) && (Ty < kInf))
+          u = (Tx + Ty + std::sqrt(2 * (C * C) - ((Tx - Ty) * (Tx - Ty)))) / 2;
+        else
+          u = std::fmin(Tx, Ty) + C;
+        if (u < r.T[k]) {
+          if (r.T[k] == kInf) {
+            first[k] = r.order.size();
+            r.order.push_back(kg);
+            r.st[k] = 2;
+            ++r.band;
+          }
+          r.T[k] = u;
+          heap.push_back({u, first[k], k});
+          std::push_heap(heap.begin(), heap.end(), later);
+        }
       }
     }
+    if (short_box && !(bx[0] == 0 && bx[1] == 0 && bx[2] == nx_ - 1 && bx[3] == ny_ - 1)) {
+      r.bx[0] = r.bx[1] = 0;
+      r.bx[2] = (int64_t)nx_ - 1;
+      r.bx[3] = (int64_t)ny_ - 1;
+      continue;
+    }
+    return r;
   }
-  // install: host mirror (whole), device map, states, band and propagated list
-  total_cost_.swap(T);
+}
+
+// computeTotalCostMap's exit replayed exactly on the host (hostFmm) over the region
+// box -- when the values cannot decide the reference's order at the exit (near ties,
+// degenerate ties) or the band replay hit its work bound.  The map, the node states,
+// the band (insertion order) and global_propagated_nodes become the reference's.
+bool DyMuPathPlanner::exactEarlyExit(unsigned si, unsigned sj, const int64_t box[4]) {
+  const uint64_t n = (uint64_t)nx_ * ny_;
+  HostFmm r = hostFmm(si, sj, box);
+  const int64_t* bx = r.bx;
+  std::fill(total_cost_.begin(), total_cost_.end(), kInf);
+  node_state_.assign(n, 0);
+  for (int64_t j = bx[1]; j <= bx[3]; ++j)
+    for (int64_t i = bx[0]; i <= bx[2]; ++i) {
+      const uint64_t k = (uint64_t)((j - bx[1]) * r.W + (i - bx[0]));
+      const uint64_t kg = idx((unsigned)i, (unsigned)j);
+      total_cost_[kg] = r.T[k];
+      node_state_[kg] = r.st[k] == 1 ? 1 : 0;
+    }
   std::fill(blk_ok_.begin(), blk_ok_.end(), 1);
   blk_missing_ = 0;
   if (dymu_memcpy_h2d(ctx_, dT_, total_cost_.data(), sizeof(double) * n) != DYMU_OK)
     throw std::runtime_error(std::string("dymu: total-cost upload failed: ") +
                              dymu_last_error(ctx_));
-  node_state_.swap(closed);
   band_cells_.clear();
   band_unordered_ = false;
+  band_values_checked_ = true;
   open_at_limit_.clear();
-  for (const uint64_t k : order)
-    if (in_band[k]) band_cells_.push_back(k);  // the reference's band vector, in order
-  propagated_extra_.swap(order);
+  for (const uint64_t kg : r.order)
+    if (!node_state_[kg]) band_cells_.push_back(kg);  // the reference's band vector, in order
+  propagated_extra_.swap(r.order);
   manual_list_ = true;
   solved_ = false;
-  return band > 0;  // :399-407
+  return r.band > 0;  // :399-407
+}
+
+// global_propagated_nodes (:447, :537-545) after a GPU solve: every reached node in
+// the order the reference inserted it, rebuilt from the values like the band's order
+// (pop_order.hpp) but for all nodes at once -- the popped (CLOSED) nodes ranked by value,
+// equal values by insertion; a node's insertion keyed by the rank of its first-popped
+// neighbour (its least CLOSED one) and its slot in that neighbour's nb4 list.  Near ties
+// (TieGuard) or an undetermined order: the reference's FMM is replayed on the host for
+// the order (hostFmm; its values are not installed).
+std::vector<uint64_t> DyMuPathPlanner::insertionOrder() {
+  fetchAll();
+  const uint64_t n = (uint64_t)nx_ * ny_;
+  const double* t = total_cost_.data();
+  const uint64_t g = idx(goal_i_, goal_j_);
+  std::vector<uint64_t> reached;
+  for (uint64_t k = 0; k < n; ++k)
+    if (t[k] < kInf) reached.push_back(k);
+  // the constant-speed radius around the goal (TieGuard): mirror ties trusted within
+  const double f0 = speed_[g];
+  double d2 = kInf;
+  for (uint64_t k = 0; k < n; ++k)
+    if (speed_[k] != f0) {
+      const double di = (double)(k % nx_) - goal_i_, dj = (double)(k / nx_) - goal_j_;
+      d2 = std::fmin(d2, di * di + dj * dj);
+    }
+  TieGuard guard(nx_, goal_i_, goal_j_, f0, std::sqrt(d2));
+  std::vector<std::pair<double, uint64_t>> popped;
+  for (const uint64_t k : reached)
+    if (closedCell(k)) popped.push_back({t[k], k});
+  std::sort(popped.begin(), popped.end());
+  std::vector<uint64_t> rank(n, ~0ull);
+  bool undetermined = popped.empty() || popped[0].second != g;
+  // x's first-popped neighbour (least value, equal ones by rank) and x's slot in its list;
+  // false when none is ranked (x ties with its least neighbour: undetermined)
+  auto first_popped = [&](uint64_t x, uint64_t& key) {
+    const unsigned i = (unsigned)(x % nx_), j = (unsigned)(x / nx_);
+    uint64_t nb[4];
+    int slot[4], m = 0;  // x's slot in nb's list: (i,j-1) sees x as its (i,j+1): 3, ...
+    if (j > 0) nb[m] = x - nx_, slot[m++] = 3;
+    if (i > 0) nb[m] = x - 1, slot[m++] = 2;
+    if (i + 1 < nx_) nb[m] = x + 1, slot[m++] = 1;
+    if (j + 1 < ny_) nb[m] = x + nx_, slot[m++] = 0;
+    int best = -1;
+    for (int q = 0; q < m; ++q) {
+      if (rank[nb[q]] == ~0ull) continue;
+      if (best < 0) {
+        best = q;
+        continue;
+      }
+      const int c = guard.cmp(nb[q], t[nb[q]], nb[best], t[nb[best]]);
+      if (c < 0 || (c == 0 && rank[nb[q]] < rank[nb[best]])) best = q;
+    }
+    if (best < 0) return false;
+    if (guard.cmp(nb[best], t[nb[best]], x, t[x]) >= 0) return false;
+    key = rank[nb[best]] * 4 + (uint64_t)slot[best];
+    return true;
+  };
+  // pop ranks: value order; a group of equal values in insertion order
+  uint64_t next = 0;
+  std::vector<std::pair<uint64_t, uint64_t>> grp;
+  for (size_t a = 0; a < popped.size() && !undetermined;) {
+    size_t b = a + 1;
+    while (b < popped.size() && popped[b].first == popped[a].first) ++b;
+    if (a > 0) (void)guard.cmp(popped[a - 1].second, popped[a - 1].first, popped[a].second,
+                               popped[a].first);
+    grp.clear();
+    for (size_t q = a; q < b; ++q) {
+      const uint64_t x = popped[q].second;
+      if (q > a) (void)guard.cmp(popped[a].second, popped[a].first, x, popped[q].first);
+      uint64_t key = 0;
+      if (x != g && !first_popped(x, key)) undetermined = true;
+      grp.push_back({x == g ? 0 : key + 1, x});
+    }
+    std::sort(grp.begin(), grp.end());
+    for (const auto& e : grp) rank[e.second] = next++;
+    a = b;
+  }
+  std::vector<std::pair<uint64_t, uint64_t>> ins;  // (key, cell)
+  ins.reserve(reached.size());
+  for (const uint64_t x : reached) {
+    if (undetermined) break;
+    uint64_t key = 0;
+    if (x != g && !first_popped(x, key)) undetermined = true;
+    ins.push_back({x == g ? 0 : key + 1, x});
+  }
+  std::vector<uint64_t> order;
+  if (undetermined || guard.near > 0) {  // the reference's own order, replayed
+    const int64_t none[4] = {0, 0, -1, -1};
+    const bool early = closed_limit_ < kInf && have_start_;
+    HostFmm r = hostFmm(early ? (int64_t)start_i_ : -1, early ? (int64_t)start_j_ : -1,
+                        early ? exit_box_ : none);
+    order.swap(r.order);
+  } else {
+    std::sort(ins.begin(), ins.end());
+    order.reserve(ins.size());
+    for (const auto& e : ins) order.push_back(e.second);
+  }
+  return order;
+}
+
+void DyMuPathPlanner::copyNodeStates(uint8_t* out) {
+  const uint64_t n = (uint64_t)nx_ * ny_;
+  if (!node_state_.empty()) {
+    std::memcpy(out, node_state_.data(), n);
+    return;
+  }
+  fetchAll();
+  for (uint64_t k = 0; k < n; ++k) out[k] = closedCell(k) ? 1 : 0;
 }
 
 // :443-468
@@ -1448,6 +1712,7 @@ void DyMuPathPlanner::resetTotalCostMap() {
   closed_limit_ = 0.0;
   band_cells_.clear();
   band_unordered_ = false;
+  band_values_checked_ = true;
   open_at_limit_.clear();
   node_state_.assign(total_cost_.size(), 0);
   propagated_extra_.clear();
@@ -1466,6 +1731,7 @@ void DyMuPathPlanner::materializeStates() {
 
 void DyMuPathPlanner::setGlobalNodeState(unsigned i, unsigned j, node_state s) {
   if (i >= nx_ || j >= ny_) return;
+  settleBand();
   materializeStates();
   node_state_[idx(i, j)] = s == CLOSED ? 1 : 0;
 }
@@ -1474,6 +1740,7 @@ void DyMuPathPlanner::setGlobalNodeState(unsigned i, unsigned j, node_state s) {
 // of device blocks can overwrite what this writes)
 void DyMuPathPlanner::propagateGlobalNode(unsigned i, unsigned j) {
   if (i >= nx_ || j >= ny_) return;
+  settleBand();
   orderBand();  // from the solve's values, before this changes any
   fetchAll();
   const uint64_t k = idx(i, j);
@@ -1525,17 +1792,19 @@ uint64_t DyMuPathPlanner::globalPropagatedCount() {
   return c - propagated_extra_.size();
 }
 
+// the reached nodes in the reference's insertion order (insertionOrder: rebuilt from
+// the values, or replayed on the host when they cannot decide it), then those
+// propagateGlobalNode added since, in the order it added them
 std::vector<globalNode> DyMuPathPlanner::globalPropagatedNodes() {
   std::vector<globalNode> out;
   if (!manual_list_) {
-    fetchAll();
     std::vector<uint8_t> extra;
     if (!propagated_extra_.empty()) {
       extra.assign(total_cost_.size(), 0);
       for (const uint64_t k : propagated_extra_) extra[k] = 1;
     }
-    for (uint64_t k = 0; k < total_cost_.size(); ++k)
-      if (total_cost_[k] < kInf && (extra.empty() || !extra[k])) out.push_back(*snapshot(k));
+    for (const uint64_t k : insertionOrder())
+      if (extra.empty() || !extra[k]) out.push_back(*snapshot(k));
   }
   for (const uint64_t k : propagated_extra_) out.push_back(*snapshot(k));
   return out;
@@ -1549,8 +1818,33 @@ std::vector<globalNode> DyMuPathPlanner::globalNarrowband() {
   return out;
 }
 
+// The band's values after a GPU early exit are the reference's update arithmetic on the
+// engine's CLOSED values: equal to the reference's within rounding, so the order of
+// minCostGlobalNode's pops is decided by them only if no two are near-tied (TieGuard).
+// Checked once, before the first pop or change of the band (it costs a sort); on a near
+// tie the exit is replayed exactly on the host and the band and its values become the
+// reference's.
+void DyMuPathPlanner::settleBand() {
+  if (band_values_checked_) return;
+  band_values_checked_ = true;
+  if (band_cells_.size() < 2) return;
+  const uint64_t g = idx(goal_i_, goal_j_);
+  TieGuard guard(nx_, goal_i_, goal_j_, speed_[g], exit_r_const_);
+  std::vector<std::pair<double, uint64_t>> bv(band_cells_.size());
+  for (size_t q = 0; q < bv.size(); ++q) bv[q] = {T(band_cells_[q]), band_cells_[q]};
+  std::sort(bv.begin(), bv.end());
+  for (size_t q = 1; q < bv.size(); ++q)
+    (void)guard.cmp(bv[q - 1].second, bv[q - 1].first, bv[q].second, bv[q].first);
+  early_info_.near_ties += guard.near;
+  if (guard.near) {
+    early_info_.exact_replay = 1;
+    (void)exactEarlyExit(start_i_, start_j_, exit_box_);
+  }
+}
+
 // :548-567 (first strict minimum, then erased from the band)
 std::optional<globalNode> DyMuPathPlanner::minCostGlobalNode() {
+  settleBand();
   if (band_cells_.empty()) return std::nullopt;
   orderBand();
   size_t best = 0;
@@ -1571,6 +1865,7 @@ std::optional<globalNode> DyMuPathPlanner::minCostGlobalNode() {
 void DyMuPathPlanner::resetGlobalNarrowBand() {
   band_cells_.clear();
   band_unordered_ = false;
+  band_values_checked_ = true;
   if (!has_goal_ || nx_ == 0) return;
   const uint64_t k = idx(goal_i_, goal_j_);
   (void)T(k);  // the goal's block in the host mirror before the write
@@ -1588,6 +1883,7 @@ bool DyMuPathPlanner::loadTotalCostMap(const double* Tin) {
   closed_limit_ = kInf;
   band_cells_.clear();
   band_unordered_ = false;
+  band_values_checked_ = true;
   open_at_limit_.clear();
   node_state_.clear();
   propagated_extra_.clear();

@@ -215,6 +215,16 @@ int dymu_planner_last_early_exit(dymu_planner* p, double out[6]) {
   return DYMU_OK;
 }
 
+int dymu_planner_last_early_exit_ex(dymu_planner* p, double* out, uint32_t n) {
+  if (!p || (n && !out)) return DYMU_ERR_ARG;
+  const auto& e = p->pl.lastEarlyExitInfo();
+  const double v[8] = {(double)e.tied,           (double)e.open_at_limit, (double)e.exact_replay,
+                       e.resolve_ms,             (double)e.replay_updates, (double)e.band_exact,
+                       (double)e.near_ties,      (double)e.replay_threads};
+  for (uint32_t q = 0; q < n && q < 8; ++q) out[q] = v[q];
+  return DYMU_OK;
+}
+
 int dymu_planner_last_solve_kind(dymu_planner* p) {
   if (!p) return DYMU_ERR_ARG;
   return p->pl.lastSolveKind();
@@ -343,6 +353,14 @@ int64_t dymu_planner_global_propagated_nodes(dymu_planner* p, uint32_t* ij, int6
     return DYMU_OK;
   });
   return rc < 0 ? rc : n;
+}
+
+int dymu_planner_get_node_states(dymu_planner* p, uint8_t* out) {
+  if (!p || !out) return DYMU_ERR_ARG;
+  return guarded([&] {
+    p->pl.copyNodeStates(out);
+    return (int)DYMU_OK;
+  });
 }
 
 int dymu_planner_reset_total_cost_map(dymu_planner* p) {

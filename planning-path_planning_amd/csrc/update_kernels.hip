@@ -332,6 +332,71 @@ __global__ void k_early_mask(const double* F, double* T, int64_t ld, uint32_t nx
   }
 }
 
+// The early exit's region (dymu_region_stats): over every cell, the bounding box of
+// those with T <= thr (out[0..3]: min i, min j, max i, max j; nothing: min > max) and
+// the number with lo <= T <= hi (out[4]) -- the engine's near ties with the exit value.
+// Wave reductions, then one atomic per wave and word.
+__global__ void k_region_box(const double* T, int64_t ld, uint32_t nx, uint32_t ny, double thr,
+                             double lo, double hi, unsigned long long* out) {
+  const uint64_t n = (uint64_t)nx * ny;
+  unsigned long long mi = ~0ull, mj = ~0ull, xi = 0, xj = 0, cnt = 0;
+  bool any = false;
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t j = c / nx, i = c % nx;
+    const double t = T[(int64_t)j * ld + (int64_t)i];
+    if (t <= thr) {
+      any = true;
+      mi = i < mi ? i : mi;
+      mj = j < mj ? j : mj;
+      xi = i > xi ? i : xi;
+      xj = j > xj ? j : xj;
+    }
+    cnt += (t >= lo && t <= hi) ? 1u : 0u;
+  }
+  if (!any) xi = xj = 0;
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a = __shfl_xor(mi, o), b = __shfl_xor(mj, o);
+    const unsigned long long e = __shfl_xor(xi, o), f = __shfl_xor(xj, o);
+    mi = a < mi ? a : mi;
+    mj = b < mj ? b : mj;
+    xi = e > xi ? e : xi;
+    xj = f > xj ? f : xj;
+    cnt += __shfl_xor(cnt, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (mi != ~0ull) {
+      atomicMin(&out[0], mi);
+      atomicMin(&out[1], mj);
+      atomicMax(&out[2], xi);
+      atomicMax(&out[3], xj);
+    }
+    if (cnt) atomicAdd(&out[4], cnt);
+  }
+}
+
+// The constant-speed radius (dymu_region_stats): the least squared distance from the
+// goal (gi, gj) to a cell whose speed differs from f0 (an obstacle included) -> *out
+__global__ void k_const_radius(const double* F, int64_t ld, uint32_t nx, uint32_t ny, uint32_t gi,
+                               uint32_t gj, double f0, unsigned long long* out) {
+  const uint64_t n = (uint64_t)nx * ny;
+  unsigned long long m = ~0ull;
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t j = c / nx, i = c % nx;
+    if (F[(int64_t)j * ld + (int64_t)i] != f0) {
+      const int64_t di = (int64_t)i - gi, dj = (int64_t)j - gj;
+      const unsigned long long d2 = (unsigned long long)(di * di + dj * dj);
+      m = d2 < m ? d2 : m;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a = __shfl_xor(m, o);
+    m = a < m ? a : m;
+  }
+  if ((threadIdx.x & 63) == 0 && m != ~0ull) atomicMin(out, m);
+}
+
 // *p = v (a per-call device scalar initialised in stream order, without a host copy)
 __global__ void k_store_u64(unsigned long long* p, unsigned long long v) {
   if (threadIdx.x == 0) *p = v;
@@ -372,6 +437,26 @@ hipError_t launch_scatter(double* T, int64_t ld, uint32_t nx, const uint64_t* id
   if (b > 4096) b = 4096;
   if (b == 0) return hipSuccess;
   hipLaunchKernelGGL(k_scatter, dim3((unsigned)b), dim3(256), 0, st, T, ld, nx, idx, vals, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_region_box(const double* T, int64_t ld, uint32_t nx, uint32_t ny, double thr,
+                             double lo, double hi, unsigned long long* out, hipStream_t st) {
+  uint64_t b = ((uint64_t)nx * ny + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b == 0) b = 1;
+  hipLaunchKernelGGL(k_region_box, dim3((unsigned)b), dim3(256), 0, st, T, ld, nx, ny, thr, lo,
+                     hi, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_const_radius(const double* F, int64_t ld, uint32_t nx, uint32_t ny, uint32_t gi,
+                               uint32_t gj, double f0, unsigned long long* out, hipStream_t st) {
+  uint64_t b = ((uint64_t)nx * ny + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b == 0) b = 1;
+  hipLaunchKernelGGL(k_const_radius, dim3((unsigned)b), dim3(256), 0, st, F, ld, nx, ny, gi, gj, f0,
+                     out);
   return hipGetLastError();
 }
 

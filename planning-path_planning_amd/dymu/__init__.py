@@ -75,6 +75,11 @@ class DymuCostState(ctypes.Structure):
     _fields_ = [(f, ctypes.c_void_p) for f in FIELDS]
 
 
+class DymuRegion(ctypes.Structure):
+    _fields_ = [("i0", ctypes.c_uint32), ("j0", ctypes.c_uint32), ("i1", ctypes.c_uint32),
+                ("j1", ctypes.c_uint32), ("n_range", ctypes.c_uint64), ("r_const", ctypes.c_double)]
+
+
 class DymuStats(ctypes.Structure):
     _fields_ = [
         ("passes", ctypes.c_uint64),
@@ -155,6 +160,9 @@ FIM_SYMBOLS = {
     "dymu_early_exit_mask": (_i32, [_vp, _vp, _vp, _u32, _u32, _u64, ctypes.c_double, _vp, _u64,
                                     ctypes.POINTER(_u64), _vp]),
     "dymu_scatter": (_i32, [_vp, _vp, _u32, _u64, _vp, _vp, _u64, _vp]),
+    "dymu_region_stats": (_i32, [_vp, _vp, _vp, _u32, _u32, _u64, _u32, _u32, ctypes.c_double,
+                                 ctypes.c_double, ctypes.c_double, ctypes.POINTER(DymuRegion),
+                                 _vp]),
     "dymu_memcpy2d_d2h": (_i32, [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t,
                                  ctypes.c_size_t, ctypes.c_size_t]),
     "dymu_memcpy2d_h2d": (_i32, [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t,
@@ -327,6 +335,16 @@ class Engine:
         _check(self._lib.dymu_scatter(self.ctx, dT, nx, ld, idx.ctypes.data, vals.ctypes.data,
                                       idx.size, None), self.ctx)
 
+    def region_stats(self, dF: int, dT: int, nx: int, ny: int, ld: int, goal_i: int,
+                     goal_j: int, thr: float, lo: float, hi: float) -> dict:
+        """dymu_region_stats: bounding box (inclusive) of the cells with T <= thr, the
+        number with lo <= T <= hi, the distance from the goal to the nearest cell of
+        another speed."""
+        r = DymuRegion()
+        _check(self._lib.dymu_region_stats(self.ctx, dF, dT, nx, ny, ld, goal_i, goal_j, thr, lo,
+                                           hi, ctypes.byref(r), None), self.ctx)
+        return {"box": (r.i0, r.j0, r.i1, r.j1), "n_range": r.n_range, "r_const": r.r_const}
+
     def alloc(self, nbytes: int) -> int:
         p = _vp()
         _check(self._lib.dymu_device_alloc(self.ctx, nbytes, ctypes.byref(p)), self.ctx)
@@ -484,6 +502,8 @@ PLANNER_SYMBOLS = {
     "dymu_planner_last_stats": (_i32, [_vp, ctypes.POINTER(DymuStats)]),
     "dymu_planner_last_solve_kind": (_i32, [_vp]),
     "dymu_planner_last_early_exit": (_i32, [_vp, _dp]),
+    "dymu_planner_last_early_exit_ex": (_i32, [_vp, _vp, _u32]),
+    "dymu_planner_get_node_states": (_i32, [_vp, _vp]),
     "dymu_planner_set_hazard_density_window": (_i32, [_vp, _u32, _u32, _u32, _u32, _dp]),
     "dymu_planner_set_trafficability_window": (_i32, [_vp, _u32, _u32, _u32, _u32, _dp]),
     "dymu_planner_last_band_size": (ctypes.c_int64, [_vp]),
@@ -711,11 +731,11 @@ class Planner:
         """How the last computeTotalCostMap resolved the reference's pop order at its
         exit value: tied cells, those left OPEN, whether the exact host replay ran
         (degenerate ties only), host milliseconds of the resolution and band replay."""
-        o = np.zeros(6)
-        _check(self._lib.dymu_planner_last_early_exit(self.h, o))
+        o = np.zeros(8)
+        _check(self._lib.dymu_planner_last_early_exit_ex(self.h, o.ctypes.data, 8))
         return {"tied": int(o[0]), "open_at_limit": int(o[1]), "exact_replay": bool(o[2]),
                 "resolve_ms": float(o[3]), "replay_updates": int(o[4]),
-                "band_exact": bool(o[5])}
+                "band_exact": bool(o[5]), "near_ties": int(o[6]), "replay_threads": int(o[7])}
 
     def lastStats(self) -> dict:
         st = DymuStats()
@@ -769,6 +789,12 @@ class Planner:
     def setGlobalNodeState(self, i: int, j: int, closed: bool):
         """The public globalNode::state: CLOSED (True) or OPEN."""
         _check(self._lib.dymu_planner_set_global_node_state(self.h, i, j, 1 if closed else 0))
+
+    def nodeStates(self) -> np.ndarray:
+        """Every node's state, [ny, nx] uint8 (1 CLOSED, 0 OPEN)."""
+        out = np.empty((self.ny, self.nx), dtype=np.uint8)
+        _check(self._lib.dymu_planner_get_node_states(self.h, out.ctypes.data))
+        return out
 
     def globalPropagatedNodes(self) -> np.ndarray:
         """global_propagated_nodes (:447): (n, 2) array of (i, j)."""

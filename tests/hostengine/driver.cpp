@@ -5,6 +5,7 @@
 //   driver fail     the same with HOST_ENGINE_FAIL_D2H set: the readback must throw
 //   driver options  solve, setEngineOptions, then read the map and a path
 //   driver ties     constant cost (every distance tie), computeTotalCostMap's early exit
+//   driver order    global_propagated_nodes in the reference's insertion order
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -86,20 +87,25 @@ int main(int argc, char** argv) {
     return 0;
   }
   if (mode == "ties") {
-    // constant / two-valued cost: mirror images tie, so which cells of exactly the
-    // exit value the reference closed -- and which it reached -- depends on its
-    // insertion order (:551-568).  With the engine's values exact (this double solves
-    // with the oracle's FMM) the planner's order resolution (pop_order.hpp) and band
-    // replay must give the reference's exit state bit for bit, without the exact host
-    // replay: the whole matrix, every node state, the band in insertion order.
+    // constant / two-valued cost: values tie, so which cells of exactly the exit value
+    // the reference closed -- and which it reached -- depends on its insertion order
+    // (:551-568).  This double solves with the oracle's FMM (exact values); the planner
+    // still treats them as an engine's: mirror ties on constant speed are resolved from
+    // the values (pop_order.hpp, band replay), any other tie sends the exit to the exact
+    // host replay.  Either way the exit state must be the reference's bit for bit: the
+    // whole matrix, every node state, the band in insertion order.
+    // exact: 1 = the exact host replay must run (two-valued speed: non-mirror ties at the
+    // exit decide it), 0 = it must not (constant speed, goal far from the border:
+    // every tie a trusted mirror image), -1 = either (mirror images off the grid)
     struct Case {
       unsigned N, gi, gj, si, sj;
       bool two;
+      int exact;
     };
-    const Case cases[] = {{512, 256, 256, 102, 128, true}, {160, 80, 80, 20, 140, false},
-                          {96, 48, 48, 48, 20, false},
-                          {97, 30, 30, 60, 60, false},   {64, 2, 5, 40, 40, false},
-                          {120, 60, 60, 100, 30, true},  {90, 45, 20, 45, 70, true}};
+    const Case cases[] = {{512, 256, 256, 102, 128, true, -1}, {160, 80, 80, 20, 140, false, 0},
+                          {96, 48, 48, 48, 20, false, 0},
+                          {97, 30, 30, 60, 60, false, -1},  {64, 2, 5, 40, 40, false, -1},
+                          {120, 60, 60, 100, 30, true, -1},  {90, 45, 20, 45, 70, true, 1}};
     uint64_t bad = 0;
     for (const Case& cs : cases) {
       const unsigned N = cs.N;
@@ -147,12 +153,93 @@ int main(int argc, char** argv) {
           break;
         }
       }
+      const int exact_at_exit = p.lastEarlyExitInfo().exact_replay;
+      // minCostGlobalNode: the first strict minimum of the band in insertion order
+      // (:551-568), with the oracle's values -- near-tied band values are settled first
+      if (!want.empty()) {
+        size_t best = 0;
+        for (size_t q = 1; q < want.size(); ++q)
+          if (T[want[q].second] < T[want[best].second]) best = q;
+        const auto mn = p.minCostGlobalNode();
+        const uint64_t k = mn ? (uint64_t)mn->pose.position[1] * N + (uint64_t)mn->pose.position[0]
+                              : ~0ull;
+        if (!mn || k != want[best].second ||
+            std::memcmp(&mn->total_cost, &T[k], sizeof(double)) != 0)
+          ++cbad;
+      }
       const auto& info = p.lastEarlyExitInfo();
-      if (info.exact_replay) ++cbad;
-      std::printf("ties N=%u r=%d oracle=%d band=%llu tied=%llu open=%llu bad=%llu\n", N, (int)r,
-                  rr, (unsigned long long)band, (unsigned long long)info.tied,
-                  (unsigned long long)info.open_at_limit, (unsigned long long)cbad);
+      if (cs.exact >= 0 && exact_at_exit != cs.exact) ++cbad;
+      std::printf("ties N=%u r=%d oracle=%d band=%llu tied=%llu open=%llu near=%llu exact=%d "
+                  "bad=%llu\n", N, (int)r, rr, (unsigned long long)band,
+                  (unsigned long long)info.tied, (unsigned long long)info.open_at_limit,
+                  (unsigned long long)info.near_ties, info.exact_replay, (unsigned long long)cbad);
       if ((int)r != rr) ++cbad;
+      bad += cbad;
+    }
+    return bad == 0 ? 0 : 1;
+  }
+  if (mode == "order") {
+    // global_propagated_nodes after computeEntireTotalCostMap and after an early exit:
+    // the reached nodes in the reference's insertion order (rebuilt from the values, or
+    // replayed on the host where near ties leave them undecided) against the oracle's
+    // recorded insertion sequence
+    struct Case {
+      unsigned N, gi, gj;
+      int si, sj;  // -1: full solve
+      int kind;    // 0 random U(1,5) + 3% obstacles, 1 constant, 2 two-valued
+    };
+    const Case cases[] = {{96, 40, 50, -1, -1, 0}, {96, 40, 50, 80, 20, 0}, {64, 32, 32, -1, -1, 1},
+                          {80, 30, 41, 60, 60, 1}, {72, 36, 36, -1, -1, 2}, {72, 20, 50, 50, 20, 2}};
+    uint64_t bad = 0;
+    for (const Case& cs : cases) {
+      const unsigned N = cs.N;
+      std::vector<std::vector<double>> cost(N, std::vector<double>(N, 1.0));
+      std::vector<double> F((uint64_t)N * N, 1.0), T((uint64_t)N * N);
+      std::vector<double> u((uint64_t)N * N), u2((uint64_t)N * N);
+      oracle_fill_u01(u.data(), u.size(), 5);
+      oracle_fill_u01(u2.data(), u2.size(), 6);
+      for (unsigned j = 0; j < N; ++j)
+        for (unsigned i = 0; i < N; ++i) {
+          const uint64_t k = (uint64_t)j * N + i;
+          const bool near_goal = i + 1 >= cs.gi && i <= cs.gi + 1 && j + 1 >= cs.gj && j <= cs.gj + 1;
+          const bool near_start = cs.si >= 0 && i + 1 >= (unsigned)cs.si && i <= (unsigned)cs.si + 1 &&
+                                  j + 1 >= (unsigned)cs.sj && j <= (unsigned)cs.sj + 1;
+          double v = 1.0;
+          if (cs.kind == 0) v = (u2[k] < 0.03 && !near_goal && !near_start) ? -1.0 : 1.0 + 4.0 * u[k];
+          if (cs.kind == 2) v = u[k] < 0.5 ? 1.0 : 2.0;
+          cost[j][i] = v;
+          F[k] = v > 0 ? v : INFINITY;
+        }
+      DyMuPathPlanner p(1.0, 2.0, 5.0, CONSERVATIVE);
+      p.initGlobalLayer(1.0, 0.5, N, N, {0.0, 0.0});
+      p.setCostMap(cost);
+      if (!p.setGoal(wp(cs.gi, cs.gj))) return 2;
+      if (cs.si < 0)
+        p.computeEntireTotalCostMap();
+      else
+        p.computeTotalCostMap(wp(cs.si, cs.sj));
+      std::vector<uint8_t> closed((uint64_t)N * N);
+      std::vector<uint64_t> seq((uint64_t)N * N);
+      oracle_fmm_order(F.data(), N, N, cs.gi, cs.gj, cs.si, cs.sj, T.data(), closed.data(),
+                       seq.data());
+      std::vector<std::pair<uint64_t, uint64_t>> want;
+      for (uint64_t k = 0; k < T.size(); ++k)
+        if (T[k] < INFINITY) want.push_back({seq[k], k});
+      std::sort(want.begin(), want.end());
+      const auto got = p.globalPropagatedNodes();
+      uint64_t cbad = got.size() != want.size();
+      for (size_t q = 0; q < got.size() && q < want.size() && !cbad; ++q) {
+        const uint64_t k =
+            (uint64_t)got[q].pose.position[1] * N + (uint64_t)got[q].pose.position[0];
+        if (k != want[q].second) {
+          std::printf("  first difference at %zu: (%u,%u) vs (%u,%u)\n", q, (unsigned)(k % N),
+                      (unsigned)(k / N), (unsigned)(want[q].second % N),
+                      (unsigned)(want[q].second / N));
+          cbad = 1;
+        }
+      }
+      std::printf("order N=%u kind=%d start=(%d,%d) reached=%zu bad=%llu\n", N, cs.kind, cs.si,
+                  cs.sj, want.size(), (unsigned long long)cbad);
       bad += cbad;
     }
     return bad == 0 ? 0 : 1;

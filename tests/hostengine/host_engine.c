@@ -163,6 +163,38 @@ int dymu_find_equal(dymu_ctx* c, const double* T, uint32_t nx, uint32_t ny, uint
   *count = n;
   return DYMU_OK;
 }
+int dymu_region_stats(dymu_ctx* c, const double* F, const double* T, uint32_t nx, uint32_t ny,
+                      uint64_t ld, uint32_t gi, uint32_t gj, double thr, double lo, double hi,
+                      dymu_region* out, void* s) {
+  (void)s;
+  if (!c || !out || gi >= nx || gj >= ny) return DYMU_ERR_ARG;
+  memset(out, 0, sizeof *out);
+  uint32_t mi = UINT32_MAX, mj = UINT32_MAX, xi = 0, xj = 0;
+  const double f0 = F[(uint64_t)gj * ld + gi];
+  double d2 = INFINITY;
+  for (uint32_t j = 0; j < ny; ++j)
+    for (uint32_t i = 0; i < nx; ++i) {
+      const double t = T[(uint64_t)j * ld + i];
+      if (t <= thr) {
+        mi = i < mi ? i : mi;
+        mj = j < mj ? j : mj;
+        xi = i > xi ? i : xi;
+        xj = j > xj ? j : xj;
+      }
+      out->n_range += t >= lo && t <= hi;
+      if (F[(uint64_t)j * ld + i] != f0) {
+        const double di = (double)i - gi, dj = (double)j - gj;
+        d2 = di * di + dj * dj < d2 ? di * di + dj * dj : d2;
+      }
+    }
+  out->r_const = sqrt(d2);
+  if (mi == UINT32_MAX) {
+    out->i0 = 1;
+    return DYMU_OK;
+  }
+  out->i0 = mi, out->j0 = mj, out->i1 = xi, out->j1 = xj;
+  return DYMU_OK;
+}
 int dymu_scatter(dymu_ctx* c, double* T, uint32_t nx, uint64_t ld, const uint64_t* idx,
                  const double* v, uint64_t n, void* s) {
   (void)s;

@@ -50,6 +50,12 @@ int dymu_find_equal(dymu_ctx* c, const double* T, uint32_t nx, uint32_t ny, uint
   (void)c; (void)T; (void)nx; (void)ny; (void)ld; (void)v; (void)idx; (void)cap; (void)n; (void)st;
   NODEV;
 }
+int dymu_region_stats(dymu_ctx* c, const double* F, const double* T, uint32_t nx, uint32_t ny,
+                      uint64_t ld, uint32_t gi, uint32_t gj, double thr, double lo, double hi,
+                      dymu_region* out, void* st) {
+  (void)c; (void)F; (void)T; (void)nx; (void)ny; (void)ld; (void)gi; (void)gj; (void)thr;
+  (void)lo; (void)hi; (void)out; (void)st; NODEV;
+}
 int dymu_scatter(dymu_ctx* c, double* T, uint32_t nx, uint64_t ld, const uint64_t* idx, const double* v,
                  uint64_t n, void* st) {
   (void)c; (void)T; (void)nx; (void)ld; (void)idx; (void)v; (void)n; (void)st; NODEV;

@@ -1,0 +1,132 @@
+"""computeTotalCostMap's exit state (a6, src/DyMu_GlobalPathPlanning.cpp:364-408) on the
+GPU engine where values tie WITHOUT mirror symmetry (VERDICT r5 "do this" 2), and
+global_propagated_nodes' order after a GPU solve (:447, :537-545; "do this" 6).
+
+The engine's values are within ~1e-14 of the reference's, not equal to them, so an
+order read off them holds only where no rounding can flip it (csrc/pop_order.hpp,
+TieGuard): the planner counts every comparison of two cells' values closer than 1e-12
+(relative) -- and every exact tie that is not a mirror image about the goal inside the
+constant-speed disc -- as a near tie, and on any near tie replays the reference exactly
+on the host.  Here every exit state is compared with the oracle's exact FMM
+(oracle_fmm_order): the never-reached mask, every node state, the band in the
+reference's insertion order, the values within the parity tolerance; with the default
+engine (not exact_sqrt).
+  * two-valued speed (1 or 2 per cell) at 512^2, three starts: integer sums tie in
+    the reference and the engine breaks them by ulps -> near ties, exact replay (where
+    the exit region holds any);
+  * config-2 terrain-class costs at 4096^2 (computeCostMap), three starts: generic
+    values -> no near tie, the exit resolved from the engine's values;
+  * global_propagated_nodes at 512^2 after a full solve and an early exit: the first
+    and last 1,000 entries (and the whole list) against the oracle's sequence."""
+import numpy as np
+import pytest
+
+from gen_golden import config2_inputs
+from test_planner import _early_matches
+
+pytestmark = pytest.mark.gpu
+
+
+def _band_order(closed, Tl, seq):
+    band = (closed == 0) & np.isfinite(Tl)
+    bj, bi = np.nonzero(band)
+    return np.stack([bi, bj], 1)[np.argsort(seq[bj, bi], kind="stable")]
+
+
+def _check_exit(p, oracle, F, g, s):
+    Tl, rc, closed, seq = oracle.fmm_order(F, g, start=s)
+    assert p.computeTotalCostMap(s) == bool(rc)
+    info = p.lastEarlyExit()
+    _early_matches(p.getTotalCostMatrix(), Tl)
+    st = p.nodeStates()
+    bad = np.argwhere(st != closed)
+    assert bad.size == 0, (len(bad), bad[:8].tolist())
+    nb = p.globalNarrowband()
+    want = _band_order(closed, Tl, seq)
+    assert nb.shape == want.shape and np.array_equal(nb, want)
+    assert p.lastBandSize() == len(want)
+    if len(want):  # minCostGlobalNode: the first strict minimum in the reference's order
+        M = p.getTotalCostMatrix()
+        vals = np.array([M[y, x] for x, y in nb])
+        (i, j), t = p.minCostGlobalNode()
+        assert (i, j) == tuple(nb[int(np.argmin(vals))]) and t == vals.min()
+    return info
+
+
+def _two_valued(N, seed):
+    rng = np.random.default_rng(seed)
+    return np.where(rng.random((N, N)) < 0.5, 1.0, 2.0)
+
+
+@pytest.mark.parametrize("s", [(300, 290), (400, 80), (40, 470)])
+def test_two_valued_512(dymu, oracle, s):
+    N, g = 512, (256, 256)
+    F = _two_valued(N, 11)
+    p = dymu.Planner()
+    try:
+        p.initGlobalLayer(1.0, 0.5, N, N)
+        p.setCostMap(F)  # cost 1 or 2, no obstacle: speed = cost (:527-528)
+        assert p.setGoal(g)
+        info = _check_exit(p, oracle, F, g, s)
+        # near ties send the exit to the exact replay; without any, the values decided
+        assert bool(info["exact_replay"]) == (info["near_ties"] > 0), info
+        print("two-valued", s, info)
+    finally:
+        p.close()
+
+
+@pytest.fixture(scope="module")
+def config2(dymu, oracle):
+    N = 4096
+    elev, terr, lut, slopes = config2_inputs(N)
+    p = dymu.Planner()
+    p.initGlobalLayer(1.0, 0.5, N, N)
+    assert p.computeCostMap(lut, slopes, ["Wheel"], elev, terr)
+    st = oracle.new_state(N, N)
+    oracle.compute_cost_map(st, 1.0, lut, slopes, 1, elev, terr)
+    F = oracle.pack_speed(st["cost"], st["hazard"], st["traff"], st["is_obstacle"], res=1.0)
+    g = (3 * N // 4, 3 * N // 4)
+    assert p.setGoal(g)
+    yield p, F, g
+    p.close()
+
+
+@pytest.mark.parametrize("s", [(2900, 2990), (1700, 2300), (500, 700)])
+def test_config2_terrain_4096(config2, oracle, s):
+    p, F, g = config2
+    info = _check_exit(p, oracle, F, g, s)
+    assert not info["exact_replay"] and info["near_ties"] == 0, info
+
+
+def _order_of(oracle_seq, Tl):
+    fin = np.isfinite(Tl)
+    jj, ii = np.nonzero(fin)
+    o = np.argsort(oracle_seq[jj, ii], kind="stable")
+    return np.stack([ii[o], jj[o]], 1)
+
+
+@pytest.mark.parametrize("start", [None, (60, 420)])
+def test_propagated_nodes_order_512(dymu, oracle, start):
+    N, g = 512, (256, 256)
+    F = oracle.synth_speed(N, N, seed=5, obst_frac=0.02, obst_seed=6, goal=g)
+    if start is not None:
+        F[start[1] - 1:start[1] + 2, start[0] - 1:start[0] + 2] = 2.0  # a safe start
+    cost = np.where(np.isfinite(F), F, -1.0)
+    p = dymu.Planner()
+    try:
+        p.initGlobalLayer(1.0, 0.5, N, N)
+        p.setCostMap(cost)
+        assert p.setGoal(g)
+        if start is None:
+            assert p.computeEntireTotalCostMap()
+        else:
+            assert p.computeTotalCostMap(start)
+        Tl, _, _, seq = oracle.fmm_order(F, g, start=start)
+        want = _order_of(seq, Tl)
+        got = p.globalPropagatedNodes()
+        assert got.shape == want.shape
+        assert np.array_equal(got[:1000], want[:1000])
+        assert np.array_equal(got[-1000:], want[-1000:])
+        assert np.array_equal(got, want)
+    finally:
+        p.close()

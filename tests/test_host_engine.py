@@ -71,6 +71,15 @@ def test_early_exit_with_ties(driver):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def test_propagated_nodes_insertion_order(driver):
+    """global_propagated_nodes (:447, :537-545) after a solve is the reached nodes in the
+    reference's insertion order -- rebuilt from the values (random terrain, constant speed)
+    or replayed on the host where ties off the mirror images leave it undecided
+    (two-valued speed) -- after computeEntireTotalCostMap and after an early exit."""
+    r = _run(driver, "order")
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 def test_early_exit_with_ties_sanitized(tmp_path):
     """The same exit-order resolution and band replay (csrc/pop_order.hpp, replayBand)
     under AddressSanitizer + UndefinedBehaviorSanitizer."""
