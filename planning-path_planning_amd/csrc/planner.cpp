@@ -808,7 +808,12 @@ bool DyMuPathPlanner::propagate(bool early, unsigned si, unsigned sj) {
   const double ms_order =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   // an undetermined or near-tied order: the exact host replay decides the exit
-  bool exact = po.degenerate() || guard.near > 0;
+  // (DYMU_EXACT_EXIT=1 forces it: measurement and tests of that path)
+  static const bool force_exact = [] {
+    const char* kv = std::getenv("DYMU_EXACT_EXIT");
+    return kv && std::atoi(kv) != 0;
+  }();
+  bool exact = po.degenerate() || guard.near > 0 || force_exact;
   // the band with the cells the reference left OPEN at t_closed: they join it, and
   // a neighbour of theirs stays in it only if it has another CLOSED neighbour
   // (otherwise it was never reached: +inf)
