@@ -129,6 +129,12 @@ struct dymu_ctx {
   // kernel 5 edge columns (PassArgs::ec): 32 doubles per 16x16 tile; 1.5-2% per
   // 16384^2 solve against the per-row W / E halo loads (profiles/r03/ec)
   int use_ec = 1;
+  // device memory kinds (dev_alloc): the maps (dymu_device_alloc, host-solve staging):
+  // uncached -- a pass's write-backs leave no dirty L2 lines for its end-of-kernel
+  // release (27.52-27.72 vs 28.06-28.28 ms per 16384^2 solve, profiles/r06/map_mem_ab.txt);
+  // the tile workspace: cached (uncached lists / keys / edge columns cost +0.6%).
+  // DYMU_MAP_MEM / DYMU_WS_MEM override (A/B)
+  int map_mem = 2, ws_mem = 0;
   double* d_ec = nullptr;
   uint64_t ec_cap = 0;  // tiles
   // windowed updates with increases: theta reset (0, default) or the raise front (1,
@@ -165,6 +171,19 @@ int fail_hip(dymu_ctx* c, hipError_t e, const char* what) {
     if (_e != hipSuccess) return fail_hip(ctx, _e, #expr); \
   } while (0)
 
+// Device memory by kind (A/B knobs): 0 hipMalloc (coarse-grained,
+// L2-cached), 1 fine-grained, 2 uncached (no L2: nothing dirty for a kernel's
+// end-of-pass release to write back)
+hipError_t dev_alloc(void** p, size_t bytes, int kind) {
+  if (kind == 1) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocFinegrained);
+  if (kind == 2) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+  return hipMalloc(p, bytes);
+}
+template <class P>
+hipError_t dev_alloc(P** p, size_t bytes, int kind) {
+  return dev_alloc(reinterpret_cast<void**>(p), bytes, kind);
+}
+
 int ensure_tiles(dymu_ctx* c, uint32_t ntiles, hipStream_t st) {
   if (ntiles <= c->tiles_cap) return DYMU_OK;
   if (c->d_lists) (void)hipFree(c->d_lists);
@@ -172,8 +191,8 @@ int ensure_tiles(dymu_ctx* c, uint32_t ntiles, hipStream_t st) {
   c->d_lists = nullptr;
   c->d_tile_epoch = nullptr;
   c->tiles_cap = 0;
-  HIPC(c, hipMalloc(&c->d_lists, sizeof(uint32_t) * 3ull * kShards * ntiles));
-  HIPC(c, hipMalloc(&c->d_tile_epoch, sizeof(uint32_t) * (uint64_t)ntiles));
+  HIPC(c, dev_alloc(&c->d_lists, sizeof(uint32_t) * 3ull * kShards * ntiles, c->ws_mem));
+  HIPC(c, dev_alloc(&c->d_tile_epoch, sizeof(uint32_t) * (uint64_t)ntiles, c->ws_mem));
   HIPC(c, hipMemsetAsync(c->d_tile_epoch, 0, sizeof(uint32_t) * (uint64_t)ntiles, st));
   c->tiles_cap = ntiles;
   c->epoch_base = 0;
@@ -188,7 +207,7 @@ int ensure_prio(dymu_ctx* c, uint32_t ntiles) {
   if (c->d_keys) (void)hipFree(c->d_keys);
   c->d_keys = nullptr;
   c->keys_cap = 0;
-  HIPC(c, hipMalloc(&c->d_keys, sizeof(unsigned long long) * 3ull * ntiles));
+  HIPC(c, dev_alloc(&c->d_keys, sizeof(unsigned long long) * 3ull * ntiles, c->ws_mem));
   c->keys_cap = ntiles;
   return DYMU_OK;
 }
@@ -220,8 +239,8 @@ int ensure_cells(dymu_ctx* c, uint64_t cells) {
   if (c->d_T) (void)hipFree(c->d_T);
   c->d_F = c->d_T = nullptr;
   c->cells_cap = 0;
-  HIPC(c, hipMalloc(&c->d_F, sizeof(double) * cells));
-  HIPC(c, hipMalloc(&c->d_T, sizeof(double) * cells));
+  HIPC(c, dev_alloc(&c->d_F, sizeof(double) * cells, c->map_mem));
+  HIPC(c, dev_alloc(&c->d_T, sizeof(double) * cells, c->map_mem));
   c->cells_cap = cells;
   return DYMU_OK;
 }
@@ -358,7 +377,7 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
       if (c->d_ec) (void)hipFree(c->d_ec);
       c->d_ec = nullptr;
       c->ec_cap = 0;
-      HIPC(c, hipMalloc(&c->d_ec, sizeof(double) * 32 * (uint64_t)ntiles));
+      HIPC(c, dev_alloc(&c->d_ec, sizeof(double) * 32 * (uint64_t)ntiles, c->ws_mem));
       c->ec_cap = ntiles;
     }
     a.ec = c->d_ec;
@@ -1144,6 +1163,8 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
       c->cu_count = prop.multiProcessorCount;
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   }
+  if (const char* kv = std::getenv("DYMU_MAP_MEM")) c->map_mem = std::atoi(kv);
+  if (const char* kv = std::getenv("DYMU_WS_MEM")) c->ws_mem = std::atoi(kv);
   if (const char* kv = std::getenv("DYMU_FIRST_BATCH"))
     c->first_batch = (uint64_t)std::max(1, std::atoi(kv));
   if (const char* kv = std::getenv("DYMU_PIPELINE")) c->pipeline = std::atoi(kv);
@@ -1492,7 +1513,7 @@ int dymu_synth_speed(dymu_ctx* c, double* dF, uint32_t nx, uint32_t ny, uint64_t
 int dymu_device_alloc(dymu_ctx* c, size_t bytes, void** p) {
   if (!c || !p) return DYMU_ERR_ARG;
   HIPC(c, hipSetDevice(c->device));
-  HIPC(c, hipMalloc(p, bytes));
+  HIPC(c, dev_alloc(p, bytes, c->map_mem));
   return DYMU_OK;
 }
 

@@ -134,3 +134,28 @@ def test_propagated_nodes_order_512(dymu, oracle, start):
         assert np.array_equal(got, want)
     finally:
         p.close()
+
+
+def test_early_exit_staircase_latency_16384(dymu):
+    """the host part of computeTotalCostMap stays bounded on the worst case
+    measured -- constant cost at 16384^2 with a 1:2 staircase exit front (3.6 M band-replay
+    updates; round 5: 0.53 s on one thread, 65 ms on 16 in round 6,
+    profiles/r06/planner_early_exit.json) -- with no near tie and no exact replay."""
+    import time
+
+    N, g, s = 16384, (8192, 8192), (11468, 9830)
+    p = dymu.Planner()
+    try:
+        p.initGlobalLayer(1.0, 0.5, N, N)
+        p.setCostMap(np.ones((N, N)))
+        assert p.setGoal(g)
+        assert p.computeTotalCostMap(s)  # warm: device buffers, host mirror registration
+        t0 = time.perf_counter()
+        assert p.computeTotalCostMap(s)
+        ms = (time.perf_counter() - t0) * 1e3
+        info = p.lastEarlyExit()
+        print("staircase 16384^2:", round(ms, 1), "ms", info)
+        assert not info["exact_replay"] and info["near_ties"] == 0 and info["band_exact"], info
+        assert info["resolve_ms"] < 400 and ms < 1000, (ms, info)
+    finally:
+        p.close()
