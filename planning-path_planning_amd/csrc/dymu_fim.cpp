@@ -134,7 +134,7 @@ struct dymu_ctx {
   // release (27.52-27.72 vs 28.06-28.28 ms per 16384^2 solve, profiles/r06/map_mem_ab.txt);
   // the tile workspace: cached (uncached lists / keys / edge columns cost +0.6%).
   // DYMU_MAP_MEM / DYMU_WS_MEM override (A/B)
-  int map_mem = 2, ws_mem = 0;
+  int map_mem = 2, ws_mem = 0, ec_mem = 0, key_mem = 0;
   double* d_ec = nullptr;
   uint64_t ec_cap = 0;  // tiles
   // windowed updates with increases: theta reset (0, default) or the raise front (1,
@@ -207,7 +207,7 @@ int ensure_prio(dymu_ctx* c, uint32_t ntiles) {
   if (c->d_keys) (void)hipFree(c->d_keys);
   c->d_keys = nullptr;
   c->keys_cap = 0;
-  HIPC(c, dev_alloc(&c->d_keys, sizeof(unsigned long long) * 3ull * ntiles, c->ws_mem));
+  HIPC(c, dev_alloc(&c->d_keys, sizeof(unsigned long long) * 3ull * ntiles, c->key_mem));
   c->keys_cap = ntiles;
   return DYMU_OK;
 }
@@ -377,7 +377,7 @@ int dom_begin(dymu_ctx* c, const double* dF, double* dT, uint32_t nx, uint32_t n
       if (c->d_ec) (void)hipFree(c->d_ec);
       c->d_ec = nullptr;
       c->ec_cap = 0;
-      HIPC(c, dev_alloc(&c->d_ec, sizeof(double) * 32 * (uint64_t)ntiles, c->ws_mem));
+      HIPC(c, dev_alloc(&c->d_ec, sizeof(double) * 32 * (uint64_t)ntiles, c->ec_mem));
       c->ec_cap = ntiles;
     }
     a.ec = c->d_ec;
@@ -1164,7 +1164,9 @@ int dymu_create(dymu_ctx** out, const dymu_opts* opts) {
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   }
   if (const char* kv = std::getenv("DYMU_MAP_MEM")) c->map_mem = std::atoi(kv);
-  if (const char* kv = std::getenv("DYMU_WS_MEM")) c->ws_mem = std::atoi(kv);
+  if (const char* kv = std::getenv("DYMU_WS_MEM")) c->ws_mem = c->ec_mem = c->key_mem = std::atoi(kv);
+  if (const char* kv = std::getenv("DYMU_EC_MEM")) c->ec_mem = std::atoi(kv);
+  if (const char* kv = std::getenv("DYMU_KEY_MEM")) c->key_mem = std::atoi(kv);
   if (const char* kv = std::getenv("DYMU_FIRST_BATCH"))
     c->first_batch = (uint64_t)std::max(1, std::atoi(kv));
   if (const char* kv = std::getenv("DYMU_PIPELINE")) c->pipeline = std::atoi(kv);

@@ -6,6 +6,7 @@
 // an N x N fp64 array exactly once with that pattern; k_write writes it the
 // same way.  Known bytes: 8 N^2 each.  Run under rocprofv3 --pmc FETCH_SIZE
 // (resp. WRITE_SIZE) and divide.
+// Usage: tools/pmc_calib [N] [uc]  (uc: uncached memory, like the product's maps)
 // Build: hipcc --offload-arch=gfx950 -O3 tools/pmc_calib.hip -o tools/pmc_calib
 #include <hip/hip_runtime.h>
 
@@ -51,8 +52,14 @@ __global__ __launch_bounds__(256) void k_write(double* a, int64_t n) {
 
 int main(int argc, char** argv) {
   const int64_t n = argc > 1 ? std::atoll(argv[1]) : 16384;
+  // "uc": the array in uncached device memory, as dymu_device_alloc's maps (round 6)
+  const bool uc = argc > 2 && argv[2][0] == 'u';
   double *a = nullptr, *sink = nullptr;
-  CK(hipMalloc(&a, sizeof(double) * n * n));
+  if (uc)
+    CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&a), sizeof(double) * n * n,
+                             hipDeviceMallocUncached));
+  else
+    CK(hipMalloc(&a, sizeof(double) * n * n));
   CK(hipMalloc(&sink, sizeof(double)));
   CK(hipMemset(a, 0, sizeof(double) * n * n));
   hipLaunchKernelGGL(k_write, dim3(4096), dim3(256), 0, 0, a, n);
