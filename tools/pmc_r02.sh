@@ -12,4 +12,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/c1" -o run -- "$R/tools/pmc_calib" 16384 ${PMC_CALIB_MEM:-uc} > "$OUT/c1.log" 2>&1 || exit 1
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/c2" -o run -- "$R/tools/pmc_calib" 16384 ${PMC_CALIB_MEM:-uc} > "$OUT/c2.log" 2>&1 || exit 1
+# the cached-memory write calibration as well: the kernel's writes are counted on a
+# cached-map pass too (tools/pmc_round.sh: w0), see tools/pmc_summary.py
+timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/c3" -o run -- "$R/tools/pmc_calib" 16384 cached > "$OUT/c3.log" 2>&1 || exit 1
 bash "$R/tools/pmc_round.sh"

@@ -10,3 +10,6 @@ for ctr in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INS
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/p$i" -o run -- python3 "$R/tools/probe1.py" $N 1 > "$OUT/p$i.log" 2>&1 || exit $?
 done
+# the writes once more with the maps in cached memory (DYMU_MAP_MEM=0): the same bytes,
+# but counted at the calibrated 8-B granularity (uncached 8-B stores count as 32-B requests)
+DYMU_MAP_MEM=0 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/w0" -o run -- python3 "$R/tools/probe1.py" $N 1 > "$OUT/w0.log" 2>&1 || exit $?

@@ -40,13 +40,30 @@ if c1 and c2:
     wf = known / calib_total(c2[0], "k_write", "WRITE_SIZE")
     calib = (f"measured on tools/pmc_calib (8-B/lane tile pattern, 2 GiB known): "
              f"FETCH_SIZE x{ff:.4f}, WRITE_SIZE x{wf:.4f}")
+# Round 6: the maps are uncached and the workspace cached, so one write factor cannot
+# fit the kernel's mixed stores (the uncached calibration counts an 8-B store as a 32-B
+# request).  With the cached-map write pass (w0) and the cached-memory calibration (c3):
+# the kernel moves the same bytes either way, so its write bytes are w0's, calibrated.
+write_per_launch = wf * write / max(n, 1)
+w0 = glob.glob(root + "/w0/run_counter_collection.csv")
+c3 = glob.glob(root + "/c3/run_counter_collection.csv")
+if w0 and c3:
+    wf0 = 8.0 * 16384 ** 2 / calib_total(c3[0], "k_write", "WRITE_SIZE")
+    w0_tot, w0_disp = 0.0, set()
+    for r in csv.DictReader(open(w0[0])):
+        if kern in r["Kernel_Name"] and r["Counter_Name"] == "WRITE_SIZE":
+            w0_tot += float(r["Counter_Value"]) * 1024.0
+            w0_disp.add(r["Dispatch_Id"])
+    write_per_launch = wf0 * w0_tot / max(len(w0_disp), 1)
+    calib += (f"; writes from the cached-map pass (DYMU_MAP_MEM=0, {len(w0_disp)} dispatches) "
+              f"x{wf0:.4f} (cached calibration): uncached 8-B stores count as 32-B requests")
 out = {
     "kernel": name, "dispatches": n, "grid": int(sys.argv[4]) if len(sys.argv) > 4 else 16384,
     "fetch_bytes_raw": fetch, "write_bytes": write,
-    "traffic_bytes_per_launch": (ff * fetch + wf * write) / max(n, 1),
+    "traffic_bytes_per_launch": ff * fetch / max(n, 1) + write_per_launch,
     "traffic_bytes_per_launch_raw": (fetch + write) / max(n, 1),
     "fetch_bytes_per_launch": ff * fetch / max(n, 1),
-    "write_bytes_per_launch": wf * write / max(n, 1),
+    "write_bytes_per_launch": write_per_launch,
     "correction": calib,
     "counters": {k: v for k, v in tot.items()},
 }
