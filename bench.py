@@ -452,7 +452,8 @@ def main():
             d = json.load(open(f))
             if d.get("kernel") and roof["kernel"] in d["kernel"] and d.get("grid", N) == N:
                 roof["traffic"] = round(d["traffic_bytes_per_launch"])
-                roof["traffic_unit"] = "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
+                roof["traffic_unit"] = ("HBM bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, "
+                                        "calibrated: " + d.get("correction", "FETCH_SIZE x2") + ")")
                 roof["traffic_source"] = os.path.basename(f)
                 break
     line = {
