@@ -104,3 +104,28 @@ def test_early_exit_with_ties_sanitized(tmp_path):
              UBSAN_OPTIONS="print_stacktrace=1")
     assert r.returncode == 0, r.stdout + r.stderr[-4000:]
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
+
+
+def test_band_replay_threads_under_tsan(tmp_path):
+    """The band replay's host threads (planner.cpp replayBand: runs of band cells from a
+    shared counter, blocks of the host mirror fetched through T()) under
+    ThreadSanitizer, 8 threads, on the tie cases (constant and two-valued maps)."""
+    if shutil.which("g++") is None:
+        pytest.skip("needs gcc/g++")
+    san = ["-g", "-O1", "-fsanitize=thread", "-ffp-contract=off", "-pthread"]
+    inc = ["-I" + os.path.join(ROOT, p) for p in ("include", "oracle",
+                                                 "planning-path_planning_amd/csrc")]
+    objs = []
+    for src in ("oracle/oracle.c", "tests/hostengine/host_engine.c"):
+        o = str(tmp_path / (os.path.basename(src) + ".o"))
+        subprocess.run(["gcc", *san, "-std=gnu11", *inc, "-c", os.path.join(ROOT, src), "-o", o],
+                       check=True)
+        objs.append(o)
+    exe = str(tmp_path / "driver_tsan")
+    srcs = [os.path.join(ROOT, s) for s in (
+        "tests/hostengine/driver.cpp", "planning-path_planning_amd/csrc/planner.cpp",
+        "planning-path_planning_amd/csrc/local_layer.cpp")]
+    subprocess.run(["g++", *san, "-std=c++17", *inc, *srcs, *objs, "-o", exe, "-lm"], check=True)
+    r = _run(exe, "ties", DYMU_HOST_THREADS="8", TSAN_OPTIONS="halt_on_error=1")
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "ThreadSanitizer" not in r.stderr
