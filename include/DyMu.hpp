@@ -347,9 +347,12 @@ class DyMuPathPlanner {
   // the reference FMM on the host (exact): until (si, sj) and its nb4 are CLOSED, or
   // the band empties for si < 0; over a box (inclusive, grown to the grid if short)
   struct HostFmm {
-    int64_t bx[4], W = 0;
-    std::vector<double> T;        // box-local, row pitch W
-    std::vector<uint8_t> st;      // 1 CLOSED, 2 in the band
+    int64_t bx[4], W = 0, PW = 0;
+    std::vector<double> T;        // the box with a one-cell ring (+inf), row pitch PW
+    std::vector<uint8_t> st;      // 1 CLOSED, 2 in the band (ring: 3 off the box, 4 off the grid)
+    uint64_t at(int64_t i, int64_t j) const {  // grid cell (i, j) inside the box
+      return (uint64_t)(j - bx[1] + 1) * (uint64_t)PW + (uint64_t)(i - bx[0] + 1);
+    }
     std::vector<uint64_t> order;  // grid indices, in first-insertion order
     uint64_t band = 0;
   };

@@ -1161,6 +1161,11 @@ void DyMuPathPlanner::orderBand() {
 // exit has a value at most t_closed, and the caller's box holds every cell the engine
 // puts below t_closed (1 + kRegionMargin) plus a ring; a pop whose neighbour lies
 // outside it means the box was short, and the replay restarts on the whole grid.
+// The box is stored with a one-cell ring at +inf: off the grid that is the reference's
+// "the other neighbour alone" (:504-523, fmin(+inf, x) = x), off the box "never
+// reached"; the ring's state says which (4: off the grid, never a neighbour; 3: outside
+// the box).  The band is an indexed 4-ary heap: a lowered value moves its cell's one
+// entry up (its sequence stays the first insertion's), so every pop is live.
 // O(m log m) for the m cells the reference reaches.
 DyMuPathPlanner::HostFmm DyMuPathPlanner::hostFmm(int64_t si, int64_t sj,
                                                   const int64_t box_in[4]) const {
@@ -1175,82 +1180,127 @@ DyMuPathPlanner::HostFmm DyMuPathPlanner::hostFmm(int64_t si, int64_t sj,
     r.bx[2] = std::min<int64_t>(nx_ - 1, box_in[2] + 2);
     r.bx[3] = std::min<int64_t>(ny_ - 1, box_in[3] + 2);
   }
+  struct E {
+    double t;
+    uint64_t seq, p;  // p: padded box-local index
+  };
+  auto less = [](const E& a, const E& b) { return a.t < b.t || (a.t == b.t && a.seq < b.seq); };
   for (;;) {
     const int64_t* bx = r.bx;
-    const int64_t W = bx[2] - bx[0] + 1, H = bx[3] - bx[1] + 1;
+    const int64_t W = bx[2] - bx[0] + 1, H = bx[3] - bx[1] + 1, PW = W + 2;
     r.W = W;
-    const uint64_t m = (uint64_t)W * (uint64_t)H;
+    r.PW = PW;
+    const uint64_t m = (uint64_t)PW * (uint64_t)(H + 2);
     r.T.assign(m, kInf);
-    r.st.assign(m, 0);  // 1 CLOSED, 2 in the band
+    r.st.assign(m, 0);  // 1 CLOSED, 2 in the band; the ring 3 / 4
+    {
+      const uint8_t s_lo = bx[1] > 0 ? 3 : 4, s_hi = bx[3] + 1 < (int64_t)ny_ ? 3 : 4;
+      const uint8_t w_lo = bx[0] > 0 ? 3 : 4, w_hi = bx[2] + 1 < (int64_t)nx_ ? 3 : 4;
+      for (int64_t c = 0; c < PW; ++c) {
+        r.st[(uint64_t)c] = s_lo;
+        r.st[(uint64_t)(H + 1) * PW + c] = s_hi;
+      }
+      for (int64_t q = 1; q <= H; ++q) {
+        r.st[(uint64_t)q * PW] = w_lo;
+        r.st[(uint64_t)q * PW + W + 1] = w_hi;
+      }
+    }
     r.order.clear();
-    std::vector<uint64_t> first(m, 0);
-    struct E {
-      double t;
-      uint64_t seq, k;  // k: box-local
-    };
-    auto later = [](const E& a, const E& b) { return a.t > b.t || (a.t == b.t && a.seq > b.seq); };
+    std::unique_ptr<uint32_t[]> pos(new uint32_t[m]);  // heap slot of each band cell
     std::vector<E> heap;
-    auto loc = [&](int64_t i, int64_t j) { return (uint64_t)((j - bx[1]) * W + (i - bx[0])); };
-    auto inbox = [&](int64_t i, int64_t j) {
-      return i >= bx[0] && j >= bx[1] && i <= bx[2] && j <= bx[3];
+    double* T = r.T.data();
+    uint8_t* st = r.st.data();
+    auto place = [&](size_t q, const E& e) {
+      heap[q] = e;
+      pos[e.p] = (uint32_t)q;
     };
-    const uint64_t g = loc(goal_i_, goal_j_);
-    r.T[g] = 0.0;
+    auto sift_up = [&](size_t q, const E e) {
+      while (q > 0) {
+        const size_t par = (q - 1) >> 2;
+        if (!less(e, heap[par])) break;
+        place(q, heap[par]);
+        q = par;
+      }
+      place(q, e);
+    };
+    auto pop_min = [&]() {
+      const E top = heap[0];
+      const E e = heap.back();
+      heap.pop_back();
+      const size_t n = heap.size();
+      if (n) {
+        size_t q = 0;
+        for (;;) {
+          const size_t c = 4 * q + 1;
+          if (c >= n) break;
+          size_t best = c;
+          const size_t ce = std::min(c + 4, n);
+          for (size_t x = c + 1; x < ce; ++x)
+            if (less(heap[x], heap[best])) best = x;
+          if (!less(heap[best], e)) break;
+          place(q, heap[best]);
+          q = best;
+        }
+        place(q, e);
+      }
+      return top;
+    };
+    const uint64_t g = r.at(goal_i_, goal_j_);
+    T[g] = 0.0;
     r.order.push_back(idx(goal_i_, goal_j_));
-    r.st[g] = 2;
+    st[g] = 2;
     heap.push_back({0.0, 0, g});
+    pos[g] = 0;
     r.band = 1;
     bool short_box = false;
     const bool early = si >= 0;
-    const uint64_t sl = early ? loc(si, sj) : 0;
+    const uint64_t sl = early ? r.at(si, sj) : 0;
     auto fully_closed = [&] {  // :424-436 (the start is interior: safeNode)
-      return early && r.st[sl] == 1 && r.st[sl - W] == 1 && r.st[sl - 1] == 1 &&
-             r.st[sl + 1] == 1 && r.st[sl + W] == 1;
+      return early && st[sl] == 1 && st[sl - PW] == 1 && st[sl - 1] == 1 && st[sl + 1] == 1 &&
+             st[sl + PW] == 1;
     };
+    const int64_t dp[4] = {-PW, -1, 1, PW};  // nb4 order (:76-80)
+    const int64_t dk[4] = {-(int64_t)nx_, -1, 1, (int64_t)nx_};
     while (r.band > 0 && !fully_closed() && !short_box) {
-      std::pop_heap(heap.begin(), heap.end(), later);
-      const E e = heap.back();
-      heap.pop_back();
-      if (r.st[e.k] != 2 || e.t != r.T[e.k]) continue;  // a superseded entry
-      r.st[e.k] = 1;
+      const uint64_t p = pop_min().p;
+      st[p] = 1;
       --r.band;
-      const int64_t i = bx[0] + (int64_t)(e.k % (uint64_t)W), j = bx[1] + (int64_t)(e.k / (uint64_t)W);
-      const int64_t nb[4][2] = {{i, j - 1}, {i - 1, j}, {i + 1, j}, {i, j + 1}};
-      for (const auto& q : nb) {
-        if (q[0] < 0 || q[1] < 0 || q[0] >= nx_ || q[1] >= ny_) continue;
-        if (!inbox(q[0], q[1])) {
+      const uint64_t row = p / (uint64_t)PW, col = p % (uint64_t)PW;
+      const uint64_t kp = (uint64_t)(bx[1] + (int64_t)row - 1) * nx_ + (uint64_t)(bx[0] + (int64_t)col - 1);
+      for (int s = 0; s < 4; ++s) {
+        const uint64_t q = p + dp[s];
+        const uint8_t sq = st[q];
+        if (sq == 1 || sq == 4) continue;
+        if (sq == 3) {
           short_box = true;  // the reference reaches beyond the box
           break;
         }
-        const uint64_t k = loc(q[0], q[1]);
-        const uint64_t kg = idx((unsigned)q[0], (unsigned)q[1]);
-        if (r.st[k] == 1 || !(F[kg] < kInf)) continue;
-        // propagateGlobalNode (:500-546) from the current values (a neighbour off the
-        // grid: the other one alone; off the box: +inf, never reached)
-        const int64_t a = q[0], b = q[1];
-        auto tt = [&](int64_t x, int64_t y) { return inbox(x, y) ? r.T[loc(x, y)] : kInf; };
-        const double Ty = (b > 0 && b + 1 < ny_) ? std::fmin(tt(a, b + 1), tt(a, b - 1))
-                          : b == 0              ? (b + 1 < ny_ ? tt(a, b + 1) : kInf)
-                                                : tt(a, b - 1);
-        const double Tx = (a > 0 && a + 1 < nx_) ? std::fmin(tt(a - 1, b), tt(a + 1, b))
-                          : a == 0              ? (a + 1 < nx_ ? tt(a + 1, b) : kInf)
-                                                : tt(a - 1, b);
-        const double C = F[kg];
+        const uint64_t kq = kp + dk[s];
+        const double C = F[kq];
+        if (!(C < kInf)) continue;
+        // propagateGlobalNode (:500-546) from the current values
+        const double Ty = std::fmin(T[q + PW], T[q - PW]);
+        const double Tx = std::fmin(T[q - 1], T[q + 1]);
         double u;
         if ((std::fabs(Tx - Ty) < C) && (Tx < kInf) && (Ty < kInf))
           u = (Tx + Ty + std::sqrt(2 * (C * C) - ((Tx - Ty) * (Tx - Ty)))) / 2;
         else
           u = std::fmin(Tx, Ty) + C;
-        if (u < r.T[k]) {
-          if (r.T[k] == kInf) {
-            first[k] = r.order.size();
-            r.order.push_back(kg);
-            r.st[k] = 2;
-            ++r.band;
-          }
-          r.T[k] = u;
-          heap.push_back({u, first[k], k});
-          std::push_heap(heap.begin(), heap.end(), later);
+        if (!(u < T[q])) continue;
+        if (T[q] == kInf) {  // first reached: into the band and the propagated list
+          const uint64_t seq = r.order.size();
+          r.order.push_back(kq);
+          st[q] = 2;
+          ++r.band;
+          T[q] = u;
+          heap.push_back({u, seq, q});
+          sift_up(heap.size() - 1, heap.back());
+        } else {
+          T[q] = u;
+          const size_t hq = pos[q];
+          E e = heap[hq];
+          e.t = u;
+          sift_up(hq, e);
         }
       }
     }
@@ -1276,7 +1326,7 @@ bool DyMuPathPlanner::exactEarlyExit(unsigned si, unsigned sj, const int64_t box
   node_state_.assign(n, 0);
   for (int64_t j = bx[1]; j <= bx[3]; ++j)
     for (int64_t i = bx[0]; i <= bx[2]; ++i) {
-      const uint64_t k = (uint64_t)((j - bx[1]) * r.W + (i - bx[0]));
+      const uint64_t k = r.at(i, j);
       const uint64_t kg = idx((unsigned)i, (unsigned)j);
       total_cost_[kg] = r.T[k];
       node_state_[kg] = r.st[k] == 1 ? 1 : 0;

@@ -86,6 +86,29 @@ int main(int argc, char** argv) {
                 (unsigned long long)info.open_at_limit, info.resolve_ms);
     return 0;
   }
+  if (mode == "exactperf") {  // the exact host replay's cost: two-valued map, far start (manual)
+    const unsigned N = argc > 2 ? (unsigned)std::atoi(argv[2]) : 2048;
+    std::vector<std::vector<double>> cost(N, std::vector<double>(N));
+    uint64_t h = 12345;
+    for (unsigned j = 0; j < N; ++j)
+      for (unsigned i = 0; i < N; ++i) {
+        h = h * 6364136223846793005ull + 1442695040888963407ull;
+        cost[j][i] = (h >> 62) ? 1.0 : 2.0;
+      }
+    DyMuPathPlanner p(1.0, 2.0, 5.0, CONSERVATIVE);
+    p.initGlobalLayer(1.0, 0.5, N, N, {0.0, 0.0});
+    p.setCostMap(cost);
+    if (!p.setGoal(wp(N / 2, N / 2))) return 2;
+    const bool r = p.computeTotalCostMap(wp(N * 0.85, N * 0.8));
+    const auto& info = p.lastEarlyExitInfo();
+    double sum = 0;
+    const auto M = p.getTotalCostMatrix();
+    for (const auto& row : M)
+      for (const double v : row) sum += v;
+    std::printf("exactperf N=%u r=%d band=%llu exact=%d resolve_ms=%.1f sum=%.17g\n", N, (int)r,
+                (unsigned long long)p.lastBandSize(), info.exact_replay, info.resolve_ms, sum);
+    return 0;
+  }
   if (mode == "ties") {
     // constant / two-valued cost: values tie, so which cells of exactly the exit value
     // the reference closed -- and which it reached -- depends on its insertion order

@@ -143,6 +143,8 @@ def test_early_exit_staircase_latency_16384(dymu):
     profiles/r06/planner_early_exit.json) -- with no near tie and no exact replay."""
     import time
 
+    if FORCED:
+        pytest.skip("the value-decided exit's latency (DYMU_EXACT_EXIT=1 forces the host replay)")
     N, g, s = 16384, (8192, 8192), (11468, 9830)
     p = dymu.Planner()
     try:
