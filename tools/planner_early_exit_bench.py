@@ -4,8 +4,10 @@ engine early exit, the host's resolution of the reference's pop order at the exi
 value (csrc/pop_order.hpp), the band replay -- on three maps per size:
   config3  U(1,5) costs with 2% obstacles (numpy; the config-3 shape),
   const    constant cost (every mirror image ties),
-  region   config3 with a constant-cost square of side N/2 around the goal.
-Goal at the centre; starts near, mid and far.  Prints one JSON object: per map
+  region   config3 with a constant-cost square of side N/2 around the goal,
+  two      costs 1 or 2 (integer sums tie in the reference; round 6),
+  int5     integer costs 1..5 with 2% obstacles (round 6).
+MAPS=two,int5 picks the maps (default config3,const,region).  Goal at the centre; starts near, mid and far.  Prints one JSON object: per map
 and start the median wall ms of 3 calls, the engine passes, the band size and
 lastEarlyExit() (tied cells, cells left OPEN at the exit value, exact replay,
 host ms).
@@ -25,6 +27,12 @@ import dymu  # noqa: E402
 def cost_map(kind, N, rng):
     if kind == "const":
         return np.ones((N, N))
+    if kind == "two":
+        return np.where(rng.random((N, N)) < 0.5, 1.0, 2.0)
+    if kind == "int5":
+        c = rng.integers(1, 6, size=(N, N)).astype(np.float64)
+        c[rng.random((N, N)) < 0.02] = -1.0
+        return c
     c = rng.uniform(1.0, 5.0, size=(N, N))
     c[rng.random((N, N)) < 0.02] = -1.0
     if kind == "region":
@@ -48,7 +56,7 @@ def main():
         rng = np.random.default_rng(5)
         g = (N // 2, N // 2)
         res = {}
-        for kind in ("config3", "const", "region"):
+        for kind in os.environ.get("MAPS", "config3,const,region").split(","):
             c = cost_map(kind, N, rng)
             c[g[1] - 1:g[1] + 2, g[0] - 1:g[0] + 2] = np.abs(c[g[1] - 1:g[1] + 2, g[0] - 1:g[0] + 2])
             p = dymu.Planner()
