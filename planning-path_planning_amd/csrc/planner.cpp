@@ -1305,6 +1305,8 @@ DyMuPathPlanner::HostFmm DyMuPathPlanner::hostFmm(int64_t si, int64_t sj,
       }
     }
     if (short_box && !(bx[0] == 0 && bx[1] == 0 && bx[2] == nx_ - 1 && bx[3] == ny_ - 1)) {
+      if (std::getenv("DYMU_ORDER_DEBUG"))
+        std::fprintf(stderr, "[dymu] exact replay: box short, restarting on the whole grid\n");
       r.bx[0] = r.bx[1] = 0;
       r.bx[2] = (int64_t)nx_ - 1;
       r.bx[3] = (int64_t)ny_ - 1;

@@ -6,6 +6,9 @@
 //   driver options  solve, setEngineOptions, then read the map and a path
 //   driver ties     constant cost (every distance tie), computeTotalCostMap's early exit
 //   driver order    global_propagated_nodes in the reference's insertion order
+//   driver exactperf N   the exact host replay's time on a two-valued N^2 map (manual)
+// HOST_ENGINE_SHORT_REGION=1 makes the double report a one-cell exit region (ties mode
+// with DYMU_EXACT_EXIT=1: the replay must restart on the whole grid)
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -191,7 +194,8 @@ int main(int argc, char** argv) {
           ++cbad;
       }
       const auto& info = p.lastEarlyExitInfo();
-      if (cs.exact >= 0 && exact_at_exit != cs.exact) ++cbad;
+      static const bool forced = std::getenv("DYMU_EXACT_EXIT") && std::atoi(std::getenv("DYMU_EXACT_EXIT"));
+      if (!forced && cs.exact >= 0 && exact_at_exit != cs.exact) ++cbad;
       std::printf("ties N=%u r=%d oracle=%d band=%llu tied=%llu open=%llu near=%llu exact=%d "
                   "bad=%llu\n", N, (int)r, rr, (unsigned long long)band,
                   (unsigned long long)info.tied, (unsigned long long)info.open_at_limit,

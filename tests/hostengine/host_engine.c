@@ -193,6 +193,10 @@ int dymu_region_stats(dymu_ctx* c, const double* F, const double* T, uint32_t nx
     return DYMU_OK;
   }
   out->i0 = mi, out->j0 = mj, out->i1 = xi, out->j1 = xj;
+  if (getenv("HOST_ENGINE_SHORT_REGION")) {  // a box short of the region: the exact replay
+    out->i0 = out->i1 = gi;                   // must notice and restart on the whole grid
+    out->j0 = out->j1 = gj;
+  }
   return DYMU_OK;
 }
 int dymu_scatter(dymu_ctx* c, double* T, uint32_t nx, uint64_t ld, const uint64_t* idx,

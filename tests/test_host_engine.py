@@ -6,7 +6,9 @@ as the solve), on CPU:
   * setEngineOptions after a solve keeps the solved map readable (map + path);
   * computeTotalCostMap's early exit on constant / two-valued maps (mirror images tie):
     the whole exit state -- matrix, node states, the band in insertion order -- equals the
-    oracle's bit for bit without the exact host replay (also under ASan / UBSan).
+    oracle's bit for bit without the exact host replay (also under ASan / UBSan);
+  * the exact host replay handed a box short of the exit region restarts on the whole
+    grid and still gives the oracle's exit state.
 Never part of the product: the product links the HIP engine, which has no CPU path."""
 import os
 import shutil
@@ -69,6 +71,22 @@ def test_engine_options_after_solve_keep_map(driver):
 def test_early_exit_with_ties(driver):
     r = _run(driver, "ties")
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_exact_replay_restarts_on_a_short_box(driver):
+    """The exact host replay runs over the exit region's box; a pop reaching past it
+    means the box was short, and the replay restarts on the whole grid (planner.cpp
+    hostFmm).  The double hands the planner a one-cell box at the goal: every exit forced
+    through the replay must still be the oracle's, bit for bit."""
+    r = _run(driver, "ties", DYMU_EXACT_EXIT="1", HOST_ENGINE_SHORT_REGION="1",
+             DYMU_ORDER_DEBUG="1")
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("ties ")]
+    assert len(lines) == 7, r.stdout
+    for ln in lines:
+        f = dict(kv.split("=") for kv in ln.split()[1:])
+        assert f["exact"] == "1" and f["bad"] == "0", ln
+    assert r.stderr.count("box short, restarting on the whole grid") >= 7, r.stderr[-2000:]
 
 
 def test_propagated_nodes_insertion_order(driver):
