@@ -1078,6 +1078,11 @@ bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& ban
     }
   };
   const uint64_t g = idx(goal_i_, goal_j_);
+  // the work bound (DYMU_REPLAY_BUDGET overrides it: tests of the overrun path)
+  static const uint64_t budget = [] {
+    const char* kv = std::getenv("DYMU_REPLAY_BUDGET");
+    return kv && std::atoll(kv) > 0 ? (uint64_t)std::atoll(kv) : kReplayBudget;
+  }();
   out.assign(band.size(), kInf);
   // threads: at least 64 band cells each; the work bound is shared out per thread
   const unsigned nt = std::max(1u, std::min(host_threads(), (unsigned)std::min<uint64_t>(
@@ -1101,7 +1106,7 @@ bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& ban
         ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       }
     } stamp{tms[t], tt0};
-    Replay rec(*this, guard, g, last, kReplayBudget / nt);
+    Replay rec(*this, guard, g, last, std::max<uint64_t>(1, budget / nt));
     for (;;) {
       const uint64_t q0 = next_run.fetch_add(run, std::memory_order_relaxed);
       if (q0 >= band.size() || rec.overrun || rec.po.degenerate()) break;
@@ -1109,7 +1114,7 @@ bool DyMuPathPlanner::replayBand(uint64_t last, const std::vector<uint64_t>& ban
       for (uint64_t q = q0; q < q1 && !rec.overrun && !rec.po.degenerate(); ++q)
         out[q] = rec.bandval((int64_t)(band[q] % nx_), (int64_t)(band[q] / nx_), 0);
     }
-    used[t] = kReplayBudget / nt - rec.budget;
+    used[t] = std::max<uint64_t>(1, budget / nt) - rec.budget;
     tg[t] = rec.guard;
     bad[t] = rec.overrun || rec.po.degenerate();
     if (rec.po.degenerate() && std::getenv("DYMU_ORDER_DEBUG")) {

@@ -194,7 +194,9 @@ int main(int argc, char** argv) {
           ++cbad;
       }
       const auto& info = p.lastEarlyExitInfo();
-      static const bool forced = std::getenv("DYMU_EXACT_EXIT") && std::atoi(std::getenv("DYMU_EXACT_EXIT"));
+      // forced through the exact replay (DYMU_EXACT_EXIT, or a band-replay budget it overruns)
+      static const bool forced = (std::getenv("DYMU_EXACT_EXIT") && std::atoi(std::getenv("DYMU_EXACT_EXIT"))) ||
+                                 std::getenv("DYMU_REPLAY_BUDGET");
       if (!forced && cs.exact >= 0 && exact_at_exit != cs.exact) ++cbad;
       std::printf("ties N=%u r=%d oracle=%d band=%llu tied=%llu open=%llu near=%llu exact=%d "
                   "bad=%llu\n", N, (int)r, rr, (unsigned long long)band,

@@ -89,6 +89,19 @@ def test_exact_replay_restarts_on_a_short_box(driver):
     assert r.stderr.count("box short, restarting on the whole grid") >= 7, r.stderr[-2000:]
 
 
+def test_band_replay_overrun_falls_back_to_exact(driver):
+    """A band replay that hits its work bound (DYMU_REPLAY_BUDGET: 4 updates here) gives
+    its values up and the exit is replayed exactly: the oracle's state bit for bit, with
+    band_exact reported through the exact flag."""
+    r = _run(driver, "ties", DYMU_REPLAY_BUDGET="4")
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("ties ")]
+    assert len(lines) == 7, r.stdout
+    for ln in lines:
+        f = dict(kv.split("=") for kv in ln.split()[1:])
+        assert f["exact"] == "1" and f["bad"] == "0", ln
+
+
 def test_propagated_nodes_insertion_order(driver):
     """global_propagated_nodes (:447, :537-545) after a solve is the reached nodes in the
     reference's insertion order -- rebuilt from the values (random terrain, constant speed)
