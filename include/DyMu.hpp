@@ -177,6 +177,8 @@ class DyMuPathPlanner {
   // reference's insertion order, then those added by propagateGlobalNode.  (At 16384^2
   // after a full solve that is ~2.6e8 snapshots: globalPropagatedCount first.)
   std::vector<globalNode> globalPropagatedNodes();
+  // the same list as grid indices (j * nx + i), without the snapshots
+  std::vector<uint64_t> globalPropagatedIndices();
   uint64_t globalPropagatedCount();
   // every node's state (ny*nx, row-major: 1 CLOSED, 0 OPEN) as the last solve or the
   // caller's setGlobalNodeState left it (the reference's globalNode::state, in bulk)

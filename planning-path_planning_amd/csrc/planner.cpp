@@ -216,6 +216,34 @@ void parallel_rows(unsigned ny, Body&& body) {
   });
 }
 
+// std::sort over up to host_threads() threads: sorted runs, merged pairwise (the merges
+// of a round in parallel).  The elements sorted here are distinct (they hold a cell
+// index), so the result is the one std::sort gives.
+template <class E>
+void parallel_sort(std::vector<E>& v) {
+  const uint64_t n = v.size();
+  const unsigned nt = std::max(1u, std::min(host_threads(), (unsigned)std::min<uint64_t>(n >> 16, 64)));
+  if (nt <= 1) {
+    std::sort(v.begin(), v.end());
+    return;
+  }
+  std::vector<uint64_t> b(nt + 1);
+  for (unsigned t = 0; t <= nt; ++t) b[t] = n * t / nt;
+  parallel_tasks(nt, [&](unsigned t) { std::sort(v.begin() + b[t], v.begin() + b[t + 1]); });
+  std::vector<E> tmp(n);
+  std::vector<E>*src = &v, *dst = &tmp;
+  for (unsigned w = 1; w < nt; w *= 2) {
+    const unsigned pairs = (nt + 2 * w - 1) / (2 * w);
+    parallel_tasks(pairs, [&](unsigned q) {
+      const unsigned lo = q * 2 * w, mid = std::min(lo + w, nt), hi = std::min(lo + 2 * w, nt);
+      std::merge(src->begin() + b[lo], src->begin() + b[mid], src->begin() + b[mid],
+                 src->begin() + b[hi], dst->begin() + b[lo]);
+    });
+    std::swap(src, dst);
+  }
+  if (src != &v) v.swap(*src);
+}
+
 }  // namespace
 
 // :145-181, with :186-210 (slope), :217-293 (nominal cost) and :297-308
@@ -1187,7 +1215,7 @@ DyMuPathPlanner::HostFmm DyMuPathPlanner::hostFmm(int64_t si, int64_t sj,
   }
   struct E {
     double t;
-    uint64_t seq, p;  // p: padded box-local index
+    uint64_t seq, p, k;  // p: padded box-local index, k: grid index
   };
   auto less = [](const E& a, const E& b) { return a.t < b.t || (a.t == b.t && a.seq < b.seq); };
   for (;;) {
@@ -1254,7 +1282,7 @@ DyMuPathPlanner::HostFmm DyMuPathPlanner::hostFmm(int64_t si, int64_t sj,
     T[g] = 0.0;
     r.order.push_back(idx(goal_i_, goal_j_));
     st[g] = 2;
-    heap.push_back({0.0, 0, g});
+    heap.push_back({0.0, 0, g, idx(goal_i_, goal_j_)});
     pos[g] = 0;
     r.band = 1;
     bool short_box = false;
@@ -1267,11 +1295,20 @@ DyMuPathPlanner::HostFmm DyMuPathPlanner::hostFmm(int64_t si, int64_t sj,
     const int64_t dp[4] = {-PW, -1, 1, PW};  // nb4 order (:76-80)
     const int64_t dk[4] = {-(int64_t)nx_, -1, 1, (int64_t)nx_};
     while (r.band > 0 && !fully_closed() && !short_box) {
-      const uint64_t p = pop_min().p;
+      const E top = pop_min();
+      const uint64_t p = top.p, kp = top.k;
       st[p] = 1;
       --r.band;
-      const uint64_t row = p / (uint64_t)PW, col = p % (uint64_t)PW;
-      const uint64_t kp = (uint64_t)(bx[1] + (int64_t)row - 1) * nx_ + (uint64_t)(bx[0] + (int64_t)col - 1);
+      if (!heap.empty()) {  // the next pop's neighbourhood, fetched while this one runs
+        const uint64_t np = heap[0].p, nk = heap[0].k;
+        const int64_t NX = (int64_t)nx_, mb = (int64_t)m - 1, ng = (int64_t)nx_ * ny_ - 1;
+        auto in = [](int64_t x, int64_t hi) { return x < 0 ? 0 : x > hi ? hi : x; };
+        const int64_t dt[8] = {-2 * PW, -PW - 1, -PW + 1, -1, 1, PW - 1, PW + 1, 2 * PW};
+        for (const int64_t d : dt) __builtin_prefetch(T + in((int64_t)np + d, mb));
+        const int64_t ds[3] = {-PW, 0, PW}, df[3] = {-NX, 0, NX};
+        for (const int64_t d : ds) __builtin_prefetch(st + in((int64_t)np + d, mb));
+        for (const int64_t d : df) __builtin_prefetch(F + in((int64_t)nk + d, ng));
+      }
       for (int s = 0; s < 4; ++s) {
         const uint64_t q = p + dp[s];
         const uint8_t sq = st[q];
@@ -1298,7 +1335,7 @@ DyMuPathPlanner::HostFmm DyMuPathPlanner::hostFmm(int64_t si, int64_t sj,
           st[q] = 2;
           ++r.band;
           T[q] = u;
-          heap.push_back({u, seq, q});
+          heap.push_back({u, seq, q, kq});
           sift_up(heap.size() - 1, heap.back());
         } else {
           T[q] = u;
@@ -1382,12 +1419,32 @@ std::vector<uint64_t> DyMuPathPlanner::insertionOrder() {
   std::vector<std::pair<double, uint64_t>> popped;
   for (const uint64_t k : reached)
     if (closedCell(k)) popped.push_back({t[k], k});
-  std::sort(popped.begin(), popped.end());
-  std::vector<uint64_t> rank(n, ~0ull);
+  parallel_sort(popped);
   bool undetermined = popped.empty() || popped[0].second != g;
+  // near ties between consecutive values first (on the host threads): any one of them
+  // leaves the pop order to the exact replay, and the keys below would be wasted (the
+  // sorted values' mean spacing falls with the cell count: from ~2^22 reached cells on
+  // generic terrain some pair lies within 1e-12 of each other)
+  {
+    const uint64_t m = popped.size();
+    const unsigned nt = std::max(1u, std::min(host_threads(), (unsigned)std::min<uint64_t>(m >> 16, 64)));
+    std::vector<uint64_t> near(nt, 0);
+    parallel_tasks(nt, [&](unsigned th) {
+      TieGuard gd(guard);
+      gd.near = 0;
+      const uint64_t q0 = std::max<uint64_t>(1, m * th / nt), q1 = m * (th + 1) / nt;
+      for (uint64_t q = q0; q < q1; ++q)
+        if (popped[q].first != popped[q - 1].first)
+          (void)gd.cmp(popped[q - 1].second, popped[q - 1].first, popped[q].second, popped[q].first);
+      near[th] = gd.near;
+    });
+    for (const uint64_t x : near) guard.near += x;
+  }
+  if (guard.near > 0) undetermined = true;
+  std::vector<uint64_t> rank(undetermined ? 0 : n, ~0ull);
   // x's first-popped neighbour (least value, equal ones by rank) and x's slot in its list;
   // false when none is ranked (x ties with its least neighbour: undetermined)
-  auto first_popped = [&](uint64_t x, uint64_t& key) {
+  auto first_popped = [&](uint64_t x, uint64_t& key, TieGuard& gd) {
     const unsigned i = (unsigned)(x % nx_), j = (unsigned)(x / nx_);
     uint64_t nb[4];
     int slot[4], m = 0;  // x's slot in nb's list: (i,j-1) sees x as its (i,j+1): 3, ...
@@ -1402,41 +1459,66 @@ std::vector<uint64_t> DyMuPathPlanner::insertionOrder() {
         best = q;
         continue;
       }
-      const int c = guard.cmp(nb[q], t[nb[q]], nb[best], t[nb[best]]);
+      const int c = gd.cmp(nb[q], t[nb[q]], nb[best], t[nb[best]]);
       if (c < 0 || (c == 0 && rank[nb[q]] < rank[nb[best]])) best = q;
     }
     if (best < 0) return false;
-    if (guard.cmp(nb[best], t[nb[best]], x, t[x]) >= 0) return false;
+    if (gd.cmp(nb[best], t[nb[best]], x, t[x]) >= 0) return false;
     key = rank[nb[best]] * 4 + (uint64_t)slot[best];
     return true;
   };
-  // pop ranks: value order; a group of equal values in insertion order
+  // pop ranks: value order; a group of equal values in insertion order (a lone value
+  // needs no key: its checks run with every node's below)
   uint64_t next = 0;
   std::vector<std::pair<uint64_t, uint64_t>> grp;
   for (size_t a = 0; a < popped.size() && !undetermined;) {
     size_t b = a + 1;
     while (b < popped.size() && popped[b].first == popped[a].first) ++b;
-    if (a > 0) (void)guard.cmp(popped[a - 1].second, popped[a - 1].first, popped[a].second,
-                               popped[a].first);
+    if (b == a + 1) {
+      rank[popped[a].second] = next++;
+      a = b;
+      continue;
+    }
     grp.clear();
     for (size_t q = a; q < b; ++q) {
       const uint64_t x = popped[q].second;
       if (q > a) (void)guard.cmp(popped[a].second, popped[a].first, x, popped[q].first);
       uint64_t key = 0;
-      if (x != g && !first_popped(x, key)) undetermined = true;
+      if (x != g && !first_popped(x, key, guard)) undetermined = true;
       grp.push_back({x == g ? 0 : key + 1, x});
     }
     std::sort(grp.begin(), grp.end());
     for (const auto& e : grp) rank[e.second] = next++;
     a = b;
   }
-  std::vector<std::pair<uint64_t, uint64_t>> ins;  // (key, cell)
-  ins.reserve(reached.size());
-  for (const uint64_t x : reached) {
-    if (undetermined) break;
-    uint64_t key = 0;
-    if (x != g && !first_popped(x, key)) undetermined = true;
-    ins.push_back({x == g ? 0 : key + 1, x});
+  popped = {};
+  // every reached node keyed by its first-popped neighbour's rank and slot, on the host
+  // threads (each with its own guard; their near ties are summed)
+  std::vector<std::pair<uint64_t, uint64_t>> ins;
+  if (!undetermined) {
+    ins.resize(reached.size());
+    const unsigned nt = std::max(
+        1u, std::min(host_threads(), (unsigned)std::min<uint64_t>(reached.size() >> 16, 64)));
+    std::vector<TieGuard> tg(nt, guard);
+    for (auto& gd : tg) gd.near = 0;
+    std::vector<uint8_t> und(nt, 0);
+    std::atomic<bool> stop{false};
+    parallel_tasks(nt, [&](unsigned th) {
+      const uint64_t q0 = reached.size() * th / nt, q1 = reached.size() * (th + 1) / nt;
+      for (uint64_t q = q0; q < q1 && !stop.load(std::memory_order_relaxed); ++q) {
+        const uint64_t x = reached[q];
+        uint64_t key = 0;
+        if (x != g && !first_popped(x, key, tg[th])) {
+          und[th] = 1;
+          stop.store(true, std::memory_order_relaxed);
+        }
+        ins[q] = {x == g ? 0 : key + 1, x};
+      }
+    });
+    for (unsigned th = 0; th < nt; ++th) {
+      guard.near += tg[th].near;
+      undetermined = undetermined || und[th];
+    }
   }
   std::vector<uint64_t> order;
   if (undetermined || guard.near > 0) {  // the reference's own order, replayed
@@ -1446,7 +1528,7 @@ std::vector<uint64_t> DyMuPathPlanner::insertionOrder() {
                         early ? exit_box_ : none);
     order.swap(r.order);
   } else {
-    std::sort(ins.begin(), ins.end());
+    parallel_sort(ins);
     order.reserve(ins.size());
     for (const auto& e : ins) order.push_back(e.second);
   }
@@ -1857,18 +1939,26 @@ uint64_t DyMuPathPlanner::globalPropagatedCount() {
 // the reached nodes in the reference's insertion order (insertionOrder: rebuilt from
 // the values, or replayed on the host when they cannot decide it), then those
 // propagateGlobalNode added since, in the order it added them
-std::vector<globalNode> DyMuPathPlanner::globalPropagatedNodes() {
-  std::vector<globalNode> out;
+std::vector<uint64_t> DyMuPathPlanner::globalPropagatedIndices() {
+  std::vector<uint64_t> out;
   if (!manual_list_) {
-    std::vector<uint8_t> extra;
+    out = insertionOrder();
     if (!propagated_extra_.empty()) {
-      extra.assign(total_cost_.size(), 0);
+      std::vector<uint8_t> extra(total_cost_.size(), 0);
       for (const uint64_t k : propagated_extra_) extra[k] = 1;
+      out.erase(std::remove_if(out.begin(), out.end(), [&](uint64_t k) { return extra[k] != 0; }),
+                out.end());
     }
-    for (const uint64_t k : insertionOrder())
-      if (extra.empty() || !extra[k]) out.push_back(*snapshot(k));
   }
-  for (const uint64_t k : propagated_extra_) out.push_back(*snapshot(k));
+  out.insert(out.end(), propagated_extra_.begin(), propagated_extra_.end());
+  return out;
+}
+
+std::vector<globalNode> DyMuPathPlanner::globalPropagatedNodes() {
+  const std::vector<uint64_t> ks = globalPropagatedIndices();
+  std::vector<globalNode> out;
+  out.reserve(ks.size());
+  for (const uint64_t k : ks) out.push_back(*snapshot(k));
   return out;
 }
 

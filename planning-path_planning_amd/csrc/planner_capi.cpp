@@ -344,11 +344,12 @@ int64_t dymu_planner_global_propagated_nodes(dymu_planner* p, uint32_t* ij, int6
       n = (int64_t)p->pl.globalPropagatedCount();
       return DYMU_OK;
     }
-    const auto nodes = p->pl.globalPropagatedNodes();
-    n = (int64_t)nodes.size();
+    const std::vector<uint64_t> ks = p->pl.globalPropagatedIndices();
+    const uint64_t nx = p->pl.sizeX();
+    n = (int64_t)ks.size();
     for (int64_t q = 0; q < n && q < max; ++q) {
-      ij[2 * q] = (uint32_t)nodes[q].pose.position[0];
-      ij[2 * q + 1] = (uint32_t)nodes[q].pose.position[1];
+      ij[2 * q] = (uint32_t)(ks[q] % nx);
+      ij[2 * q + 1] = (uint32_t)(ks[q] / nx);
     }
     return DYMU_OK;
   });

@@ -218,7 +218,9 @@ int main(int argc, char** argv) {
       int kind;    // 0 random U(1,5) + 3% obstacles, 1 constant, 2 two-valued
     };
     const Case cases[] = {{96, 40, 50, -1, -1, 0}, {96, 40, 50, 80, 20, 0}, {64, 32, 32, -1, -1, 1},
-                          {80, 30, 41, 60, 60, 1}, {72, 36, 36, -1, -1, 2}, {72, 20, 50, 50, 20, 2}};
+                          {80, 30, 41, 60, 60, 1}, {72, 36, 36, -1, -1, 2}, {72, 20, 50, 50, 20, 2},
+                          // >= 2^17 reached nodes: the sorts and the keys on several threads
+                          {600, 300, 280, -1, -1, 0}, {600, 300, 280, 520, 500, 0}};
     uint64_t bad = 0;
     for (const Case& cs : cases) {
       const unsigned N = cs.N;
@@ -256,7 +258,10 @@ int main(int argc, char** argv) {
         if (T[k] < INFINITY) want.push_back({seq[k], k});
       std::sort(want.begin(), want.end());
       const auto got = p.globalPropagatedNodes();
-      uint64_t cbad = got.size() != want.size();
+      const auto got_k = p.globalPropagatedIndices();  // the flat ABI's form: the same list
+      uint64_t cbad = got.size() != want.size() || got_k.size() != got.size();
+      for (size_t q = 0; q < got.size() && !cbad; ++q)
+        cbad = got_k[q] != (uint64_t)got[q].pose.position[1] * N + (uint64_t)got[q].pose.position[0];
       for (size_t q = 0; q < got.size() && q < want.size() && !cbad; ++q) {
         const uint64_t k =
             (uint64_t)got[q].pose.position[1] * N + (uint64_t)got[q].pose.position[0];

@@ -140,7 +140,8 @@ def test_early_exit_with_ties_sanitized(tmp_path):
 def test_band_replay_threads_under_tsan(tmp_path):
     """The band replay's host threads (planner.cpp replayBand: runs of band cells from a
     shared counter, blocks of the host mirror fetched through T()) under
-    ThreadSanitizer, 8 threads, on the tie cases (constant and two-valued maps)."""
+    ThreadSanitizer, 8 threads, on the tie cases (constant and two-valued maps); and
+    insertionOrder's threads (parallel keys and sorts) on the order cases."""
     if shutil.which("g++") is None:
         pytest.skip("needs gcc/g++")
     san = ["-g", "-O1", "-fsanitize=thread", "-ffp-contract=off", "-pthread"]
@@ -158,5 +159,9 @@ def test_band_replay_threads_under_tsan(tmp_path):
         "planning-path_planning_amd/csrc/local_layer.cpp")]
     subprocess.run(["g++", *san, "-std=c++17", *inc, *srcs, *objs, "-o", exe, "-lm"], check=True)
     r = _run(exe, "ties", DYMU_HOST_THREADS="8", TSAN_OPTIONS="halt_on_error=1")
+    assert r.returncode == 0, r.stdout + r.stderr[-4000:]
+    assert "ThreadSanitizer" not in r.stderr
+    # global_propagated_nodes' rebuild: keys and sorts on the host threads (600^2 cases)
+    r = _run(exe, "order", DYMU_HOST_THREADS="8", TSAN_OPTIONS="halt_on_error=1")
     assert r.returncode == 0, r.stdout + r.stderr[-4000:]
     assert "ThreadSanitizer" not in r.stderr
