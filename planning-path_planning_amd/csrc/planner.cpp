@@ -1197,9 +1197,76 @@ void DyMuPathPlanner::orderBand() {
 // The box is stored with a one-cell ring at +inf: off the grid that is the reference's
 // "the other neighbour alone" (:504-523, fmin(+inf, x) = x), off the box "never
 // reached"; the ring's state says which (4: off the grid, never a neighbour; 3: outside
-// the box).  The band is an indexed 4-ary heap: a lowered value moves its cell's one
-// entry up (its sequence stays the first insertion's), so every pop is live.
+// the box).  The band is a radix heap (BandQueue below); each pop prefetches the next
+// one's neighbourhood while it updates its own.
 // O(m log m) for the m cells the reference reaches.
+namespace {
+// The band in the reference's pop order -- least value, equal values by first insertion
+// -- as a radix heap on the values' bit patterns (a non-negative double orders as its
+// bits): bucket b > 0 holds the keys whose highest bit differing from the last popped
+// key is bit b - 1; `eq` (a heap on the sequence) the keys equal to it.  Every value the
+// replay inserts is at least the last popped one in exact arithmetic; one rounded below
+// it goes to `below` (a heap on value, then sequence), popped first.  A lowered value
+// is pushed again and the entry it supersedes is skipped when popped (its value is no
+// longer the cell's).
+struct BandQueue {
+  struct E {
+    uint64_t key, seq, p, k;  // value bits, first insertion, box-local index, grid index
+  };
+  std::vector<E> b[65], eq, below;
+  uint64_t last = 0;
+  static bool seq_after(const E& x, const E& y) { return x.seq > y.seq; }
+  static bool after(const E& x, const E& y) {
+    return x.key > y.key || (x.key == y.key && x.seq > y.seq);
+  }
+  void push(const E& e) {
+    if (e.key < last) {
+      below.push_back(e);
+      std::push_heap(below.begin(), below.end(), after);
+    } else if (e.key == last) {
+      eq.push_back(e);
+      std::push_heap(eq.begin(), eq.end(), seq_after);
+    } else {
+      b[64 - __builtin_clzll(e.key ^ last)].push_back(e);
+    }
+  }
+  // the entry the next pop returns (nullptr: empty); the least key's bucket is spread
+  // over the lower ones when `eq` has run dry
+  const E* next() {
+    if (!below.empty()) return &below.front();
+    if (eq.empty()) {
+      int i = 1;
+      while (i <= 64 && b[i].empty()) ++i;
+      if (i > 64) return nullptr;
+      uint64_t mn = ~0ull;
+      for (const E& e : b[i]) mn = std::min(mn, e.key);
+      last = mn;
+      std::vector<E> v;
+      v.swap(b[i]);
+      for (const E& e : v) push(e);  // each goes to a bucket below i, or to eq
+      v.clear();
+      b[i].swap(v);  // the bucket keeps its buffer
+    }
+    return &eq.front();
+  }
+  bool pop(E& out) {
+    if (!next()) return false;
+    const bool lo = !below.empty();
+    std::vector<E>& h = lo ? below : eq;
+    std::pop_heap(h.begin(), h.end(), lo ? after : seq_after);
+    out = h.back();
+    h.pop_back();
+    return true;
+  }
+};
+
+uint64_t value_bits(double t) {
+  uint64_t u;
+  std::memcpy(&u, &t, sizeof u);
+  return u;
+}
+}  // namespace
+
 DyMuPathPlanner::HostFmm DyMuPathPlanner::hostFmm(int64_t si, int64_t sj,
                                                   const int64_t box_in[4]) const {
   const double* F = speed_.data();
@@ -1213,11 +1280,6 @@ DyMuPathPlanner::HostFmm DyMuPathPlanner::hostFmm(int64_t si, int64_t sj,
     r.bx[2] = std::min<int64_t>(nx_ - 1, box_in[2] + 2);
     r.bx[3] = std::min<int64_t>(ny_ - 1, box_in[3] + 2);
   }
-  struct E {
-    double t;
-    uint64_t seq, p, k;  // p: padded box-local index, k: grid index
-  };
-  auto less = [](const E& a, const E& b) { return a.t < b.t || (a.t == b.t && a.seq < b.seq); };
   for (;;) {
     const int64_t* bx = r.bx;
     const int64_t W = bx[2] - bx[0] + 1, H = bx[3] - bx[1] + 1, PW = W + 2;
@@ -1239,51 +1301,18 @@ DyMuPathPlanner::HostFmm DyMuPathPlanner::hostFmm(int64_t si, int64_t sj,
       }
     }
     r.order.clear();
-    std::unique_ptr<uint32_t[]> pos(new uint32_t[m]);  // heap slot of each band cell
-    std::vector<E> heap;
+    // each band cell's first-insertion sequence (32 bits while the box allows)
+    const bool wide = m >= (1ull << 32);
+    std::vector<uint32_t> seq32(wide ? 0 : m);
+    std::vector<uint64_t> seq64(wide ? m : 0);
+    BandQueue band;
     double* T = r.T.data();
     uint8_t* st = r.st.data();
-    auto place = [&](size_t q, const E& e) {
-      heap[q] = e;
-      pos[e.p] = (uint32_t)q;
-    };
-    auto sift_up = [&](size_t q, const E e) {
-      while (q > 0) {
-        const size_t par = (q - 1) >> 2;
-        if (!less(e, heap[par])) break;
-        place(q, heap[par]);
-        q = par;
-      }
-      place(q, e);
-    };
-    auto pop_min = [&]() {
-      const E top = heap[0];
-      const E e = heap.back();
-      heap.pop_back();
-      const size_t n = heap.size();
-      if (n) {
-        size_t q = 0;
-        for (;;) {
-          const size_t c = 4 * q + 1;
-          if (c >= n) break;
-          size_t best = c;
-          const size_t ce = std::min(c + 4, n);
-          for (size_t x = c + 1; x < ce; ++x)
-            if (less(heap[x], heap[best])) best = x;
-          if (!less(heap[best], e)) break;
-          place(q, heap[best]);
-          q = best;
-        }
-        place(q, e);
-      }
-      return top;
-    };
     const uint64_t g = r.at(goal_i_, goal_j_);
     T[g] = 0.0;
     r.order.push_back(idx(goal_i_, goal_j_));
     st[g] = 2;
-    heap.push_back({0.0, 0, g, idx(goal_i_, goal_j_)});
-    pos[g] = 0;
+    band.push({value_bits(0.0), 0, g, idx(goal_i_, goal_j_)});
     r.band = 1;
     bool short_box = false;
     const bool early = si >= 0;
@@ -1294,13 +1323,14 @@ DyMuPathPlanner::HostFmm DyMuPathPlanner::hostFmm(int64_t si, int64_t sj,
     };
     const int64_t dp[4] = {-PW, -1, 1, PW};  // nb4 order (:76-80)
     const int64_t dk[4] = {-(int64_t)nx_, -1, 1, (int64_t)nx_};
-    while (r.band > 0 && !fully_closed() && !short_box) {
-      const E top = pop_min();
+    BandQueue::E top;
+    while (r.band > 0 && !fully_closed() && !short_box && band.pop(top)) {
       const uint64_t p = top.p, kp = top.k;
+      if (st[p] != 2 || value_bits(T[p]) != top.key) continue;  // a superseded entry
       st[p] = 1;
       --r.band;
-      if (!heap.empty()) {  // the next pop's neighbourhood, fetched while this one runs
-        const uint64_t np = heap[0].p, nk = heap[0].k;
+      if (const BandQueue::E* nx = band.next()) {  // its neighbourhood, fetched meanwhile
+        const uint64_t np = nx->p, nk = nx->k;
         const int64_t NX = (int64_t)nx_, mb = (int64_t)m - 1, ng = (int64_t)nx_ * ny_ - 1;
         auto in = [](int64_t x, int64_t hi) { return x < 0 ? 0 : x > hi ? hi : x; };
         const int64_t dt[8] = {-2 * PW, -PW - 1, -PW + 1, -1, 1, PW - 1, PW + 1, 2 * PW};
@@ -1329,21 +1359,21 @@ DyMuPathPlanner::HostFmm DyMuPathPlanner::hostFmm(int64_t si, int64_t sj,
         else
           u = std::fmin(Tx, Ty) + C;
         if (!(u < T[q])) continue;
+        uint64_t seq;
         if (T[q] == kInf) {  // first reached: into the band and the propagated list
-          const uint64_t seq = r.order.size();
+          seq = r.order.size();
+          if (wide)
+            seq64[q] = seq;
+          else
+            seq32[q] = (uint32_t)seq;
           r.order.push_back(kq);
           st[q] = 2;
           ++r.band;
-          T[q] = u;
-          heap.push_back({u, seq, q, kq});
-          sift_up(heap.size() - 1, heap.back());
         } else {
-          T[q] = u;
-          const size_t hq = pos[q];
-          E e = heap[hq];
-          e.t = u;
-          sift_up(hq, e);
+          seq = wide ? seq64[q] : seq32[q];
         }
+        T[q] = u;
+        band.push({value_bits(u), seq, q, kq});
       }
     }
     if (short_box && !(bx[0] == 0 && bx[1] == 0 && bx[2] == nx_ - 1 && bx[3] == ny_ - 1)) {
@@ -1420,7 +1450,12 @@ std::vector<uint64_t> DyMuPathPlanner::insertionOrder() {
   for (const uint64_t k : reached)
     if (closedCell(k)) popped.push_back({t[k], k});
   parallel_sort(popped);
-  bool undetermined = popped.empty() || popped[0].second != g;
+  // DYMU_EXACT_EXIT=1 sends the list to the exact replay too (tests of that path)
+  static const bool force_exact = [] {
+    const char* kv = std::getenv("DYMU_EXACT_EXIT");
+    return kv && std::atoi(kv) != 0;
+  }();
+  bool undetermined = force_exact || popped.empty() || popped[0].second != g;
   // near ties between consecutive values first (on the host threads): any one of them
   // leaves the pop order to the exact replay, and the keys below would be wasted (the
   // sorted values' mean spacing falls with the cell count: from ~2^22 reached cells on

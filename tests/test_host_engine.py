@@ -89,6 +89,15 @@ def test_exact_replay_restarts_on_a_short_box(driver):
     assert r.stderr.count("box short, restarting on the whole grid") >= 7, r.stderr[-2000:]
 
 
+def test_propagated_order_from_the_exact_replay(driver):
+    """global_propagated_nodes taken from the exact host replay (DYMU_EXACT_EXIT=1 sends
+    it there; at scale near ties do): the oracle's recorded insertion order on every
+    order case, 600^2 full solves and exits included (the replay's radix band queue)."""
+    r = _run(driver, "order", DYMU_EXACT_EXIT="1")
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    assert r.stdout.count("bad=0") == 8, r.stdout
+
+
 def test_band_replay_overrun_falls_back_to_exact(driver):
     """A band replay that hits its work bound (DYMU_REPLAY_BUDGET: 4 updates here) gives
     its values up and the exit is replayed exactly: the oracle's state bit for bit, with
