@@ -124,7 +124,7 @@ int dymu_planner_set_global_node_state(dymu_planner* p, uint32_t i, uint32_t j, 
 /* global_propagated_nodes (:447): the count (max <= 0: cheap); up to max (i, j) pairs in
  * ij, in the reference's insertion order (DyMuPathPlanner::globalPropagatedIndices) --
  * rebuilt from the values, or from the exact host replay of the reference's FMM where
- * near ties leave it open (from ~2^22 reached nodes: ~40 s for the whole list at 16384^2) */
+ * near ties leave it open (from ~2^22 reached nodes: ~34 s for the whole list at 16384^2) */
 int64_t dymu_planner_global_propagated_nodes(dymu_planner* p, uint32_t* ij, int64_t max);
 /* install a total-cost map (ny*nx, +inf unreachable) as a converged
  * computeEntireTotalCostMap leaves it (every finite node CLOSED) */

@@ -1446,16 +1446,22 @@ std::vector<uint64_t> DyMuPathPlanner::insertionOrder() {
       d2 = std::fmin(d2, di * di + dj * dj);
     }
   TieGuard guard(nx_, goal_i_, goal_j_, f0, std::sqrt(d2));
-  std::vector<std::pair<double, uint64_t>> popped;
-  for (const uint64_t k : reached)
-    if (closedCell(k)) popped.push_back({t[k], k});
-  parallel_sort(popped);
-  // DYMU_EXACT_EXIT=1 sends the list to the exact replay too (tests of that path)
+  // DYMU_EXACT_EXIT=1 sends the list to the exact replay too (tests of that path).  So
+  // does a list of more than 2^23 nodes: among that many values some two lie within 1e-12
+  // of each other (tens of such pairs are expected; none has been seen missing), so the
+  // sort below would only find that out
   static const bool force_exact = [] {
     const char* kv = std::getenv("DYMU_EXACT_EXIT");
     return kv && std::atoi(kv) != 0;
   }();
-  bool undetermined = force_exact || popped.empty() || popped[0].second != g;
+  std::vector<std::pair<double, uint64_t>> popped;
+  const bool large = reached.size() > (1ull << 23);
+  if (!force_exact && !large) {
+    for (const uint64_t k : reached)
+      if (closedCell(k)) popped.push_back({t[k], k});
+    parallel_sort(popped);
+  }
+  bool undetermined = force_exact || large || popped.empty() || popped[0].second != g;
   // near ties between consecutive values first (on the host threads): any one of them
   // leaves the pop order to the exact replay, and the keys below would be wasted (the
   // sorted values' mean spacing falls with the cell count: from ~2^22 reached cells on
